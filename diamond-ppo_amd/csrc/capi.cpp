@@ -1,0 +1,591 @@
+// libdppo C ABI: handle/workspace management and the host-side orchestration of one PPO.learn
+// (reference diamond/ppo.py:224-287, continuous_ppo.py:236-299) as a stream-ordered sequence of
+// gfx950 kernels, with RCCL collectives for the env-axis data-parallel case.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "common.h"
+
+namespace dppo {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+ParamOffsets offsets_from_layout(const dppo_dims& d, const dppo_layout& L) {
+  ParamOffsets p{};
+  const int s = d.continuous ? 1 : 0;
+  p.ls = d.continuous ? L.offset[0] : -1;
+  p.W1 = L.offset[s + 0];
+  p.b1 = L.offset[s + 1];
+  p.W2 = L.offset[s + 2];
+  p.b2 = L.offset[s + 3];
+  p.Wa = L.offset[s + 4];
+  p.ba = L.offset[s + 5];
+  p.Wo = L.offset[s + 6];
+  p.bo = L.offset[s + 7];
+  p.Wc = L.offset[s + 8];
+  p.bc = L.offset[s + 9];
+  p.Wv = L.offset[s + 10];
+  p.bv = L.offset[s + 11];
+  return p;
+}
+
+}  // namespace dppo
+
+using namespace dppo;
+
+#define DPPO_NCCL_CHECK(expr)                                                             \
+  do {                                                                                    \
+    ncclResult_t r_ = (expr);                                                             \
+    if (r_ != ncclSuccess) {                                                              \
+      set_error("%s failed: %s", #expr, ncclGetErrorString(r_));                         \
+      return DPPO_ECOMM;                                                                  \
+    }                                                                                     \
+  } while (0)
+
+struct dppo_handle {
+  int device = 0;
+  dppo_dims dims{};
+  dppo_layout layout{};
+  ParamOffsets po{};
+  MlpShape sh{};
+  bool mlp_ok = false;
+  int64_t B = 0;   // local samples T*N
+  int32_t mb = 0;  // local minibatch size B / M
+  int G = 1;       // workgroups (= gradient slabs) of the fused minibatch kernel
+  int64_t slab_stride = 0;
+  int n_partials = 0;
+  // device workspace
+  float *logp = nullptr, *values = nullptr, *next_values = nullptr, *adv = nullptr,
+        *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
+        *trace = nullptr, *mean_std = nullptr;
+  double *partials = nullptr, *dsum = nullptr;
+  int32_t* perms_dev = nullptr;
+  int32_t* perms_pinned = nullptr;
+  hipEvent_t perm_copy_done = nullptr;
+  bool perm_copy_pending = false;
+  int32_t trace_rows = 0;
+  hipStream_t last_stream = nullptr;
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+namespace {
+
+inline int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+int build_layout(const dppo_dims* d, dppo_layout* L) {
+  std::memset(L, 0, sizeof(*L));
+  const int H = d->hidden, D = d->obs_dim, A = d->act_dim;
+  int rows[DPPO_MAX_TENSORS], cols[DPPO_MAX_TENSORS];
+  int n = 0;
+  auto add = [&](int r, int c) {
+    rows[n] = r;
+    cols[n] = c;
+    ++n;
+  };
+  if (d->continuous) add(1, A);  // actor_log_std [1, A] (continuous_ppo.py:76), registered first
+  add(H, D);                     // base.0      (ppo.py:54)
+  add(H, 1);
+  add(H, H);                     // base.2      (ppo.py:56)
+  add(H, 1);
+  add(H, H);                     // actor(_mean)_head.0 (ppo.py:61)
+  add(H, 1);
+  add(A, H);                     // actor(_mean)_head.2 (ppo.py:63)
+  add(A, 1);
+  add(H, H);                     // critic_head.0 (ppo.py:68)
+  add(H, 1);
+  add(1, H);                     // critic_head.2 (ppo.py:70)
+  add(1, 1);
+  int64_t off = 0, real = 0;
+  for (int i = 0; i < n; ++i) {
+    const int64_t ne = (int64_t)rows[i] * cols[i];
+    L->offset[i] = off;
+    L->numel[i] = ne;
+    L->rows[i] = rows[i];
+    L->cols[i] = cols[i];
+    off = round_up(off + ne, 16);
+    real += ne;
+  }
+  L->count = n;
+  L->total = off;
+  L->n_real = real;
+  return DPPO_OK;
+}
+
+int validate_dims(const dppo_dims* d) {
+  if (!d) {
+    set_error("dims is NULL");
+    return DPPO_EINVAL;
+  }
+  if (d->rollout_steps < 1 || d->num_envs < 1 || d->obs_dim < 1 || d->act_dim < 1 ||
+      d->hidden < 1 || d->num_epochs < 1 || d->num_minibatches < 1 || d->world_size < 1 ||
+      d->rank < 0 || d->rank >= d->world_size) {
+    set_error("invalid dims (T=%d N=%d D=%d A=%d H=%d E=%d M=%d world=%d rank=%d)",
+              d->rollout_steps, d->num_envs, d->obs_dim, d->act_dim, d->hidden, d->num_epochs,
+              d->num_minibatches, d->world_size, d->rank);
+    return DPPO_EINVAL;
+  }
+  if ((int64_t)d->rollout_steps * d->num_envs > 0x7FFFFFFF) {
+    set_error("T*N exceeds int32 sample indexing");
+    return DPPO_EINVAL;
+  }
+  return DPPO_OK;
+}
+
+template <typename T>
+int dalloc(T** p, int64_t n) {
+  if (n <= 0) n = 1;
+  hipError_t e = hipMalloc((void**)p, (size_t)n * sizeof(T));
+  if (e != hipSuccess) {
+    set_error("hipMalloc(%lld bytes) failed: %s", (long long)(n * sizeof(T)),
+              hipGetErrorString(e));
+    return DPPO_ENOMEM;
+  }
+  return DPPO_OK;
+}
+
+#define DPPO_TRY(x)       \
+  do {                    \
+    int rc_ = (x);        \
+    if (rc_ != DPPO_OK) { \
+      return rc_;         \
+    }                     \
+  } while (0)
+
+inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+int require_mlp(const dppo_handle* h) {
+  if (!h->mlp_ok) {
+    set_error("fused MLP kernels support hidden=64, obs_dim<=32, act_dim<=16 (got H=%d D=%d A=%d)",
+              h->dims.hidden, h->dims.obs_dim, h->dims.act_dim);
+    return DPPO_EUNSUPPORTED;
+  }
+  return DPPO_OK;
+}
+
+int allreduce(dppo_handle* h, void* buf, size_t n, ncclDataType_t t, hipStream_t s) {
+  if (!h->comm || h->nranks <= 1) return DPPO_OK;
+  DPPO_NCCL_CHECK(ncclAllReduce(buf, buf, n, t, ncclSum, h->comm, s));
+  return DPPO_OK;
+}
+
+int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const dppo_hparams* hp,
+            const dppo_learn_outputs* out, hipStream_t s) {
+  DPPO_TRY(require_mlp(h));
+  if (!ro || !params || !hp || !ro->obs || !ro->next_obs || !ro->actions || !ro->rewards ||
+      !ro->term || !ro->trunc) {
+    set_error("null rollout/params/hparams pointer");
+    return DPPO_EINVAL;
+  }
+  const dppo_dims& d = h->dims;
+  // (2) old-policy evaluation (ppo.py:235-238)
+  DPPO_TRY(launch_eval(h->sh, h->po, params, ro->obs, ro->actions, ro->next_obs, h->logp,
+                       h->values, h->next_values, h->B, s));
+  // (3) GAE + returns (ppo.py:240-241)
+  DPPO_TRY(launch_gae(ro->rewards, ro->term, ro->trunc, h->values, h->next_values, h->adv, h->ret,
+                      h->partials, d.rollout_steps, d.num_envs, hp->gamma, hp->gae_lambda, s,
+                      &h->n_partials));
+  // (4) advantage statistics, global over ranks (ppo.py:243)
+  if (hp->advantage_norm) {
+    DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, s));
+    DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, s));
+  }
+  // (5) sample records for the minibatch gather (ppo.py:246-249)
+  PackArgs pa{};
+  pa.obs = ro->obs;
+  pa.actions = ro->actions;
+  pa.logp = h->logp;
+  pa.adv = h->adv;
+  pa.ret = h->ret;
+  pa.dsum = h->dsum;
+  pa.n_total = (double)h->B * (double)(h->comm ? h->nranks : 1);
+  pa.advantage_norm = hp->advantage_norm;
+  pa.adv_out = h->adv_n;
+  pa.rec = h->rec;
+  pa.B = h->B;
+  pa.D = d.obs_dim;
+  pa.D8 = h->sh.D8;
+  pa.A = d.act_dim;
+  pa.R = h->sh.R;
+  pa.continuous = d.continuous;
+  DPPO_TRY(launch_pack(pa, s));
+  if (out) {
+    const size_t nb = (size_t)h->B * sizeof(float);
+    if (out->log_probs)
+      DPPO_HIP_CHECK(hipMemcpyAsync(out->log_probs, h->logp, nb, hipMemcpyDeviceToDevice, s));
+    if (out->values)
+      DPPO_HIP_CHECK(hipMemcpyAsync(out->values, h->values, nb, hipMemcpyDeviceToDevice, s));
+    if (out->next_values)
+      DPPO_HIP_CHECK(
+          hipMemcpyAsync(out->next_values, h->next_values, nb, hipMemcpyDeviceToDevice, s));
+    if (out->advantages)
+      DPPO_HIP_CHECK(hipMemcpyAsync(out->advantages, h->adv_n, nb, hipMemcpyDeviceToDevice, s));
+    if (out->returns)
+      DPPO_HIP_CHECK(hipMemcpyAsync(out->returns, h->ret, nb, hipMemcpyDeviceToDevice, s));
+  }
+  return DPPO_OK;
+}
+
+// One minibatch: fused gradient kernel -> slab reduction -> [all-reduce] (grad left in h->grad).
+int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int32_t m,
+                   int32_t m_total, const dppo_hparams* hp, hipStream_t s) {
+  const dppo_dims& d = h->dims;
+  GradArgs ga{};
+  ga.params = params;
+  ga.rec = h->rec;
+  ga.idx = idx;
+  ga.m = m;
+  ga.inv_m = (float)(1.0 / (double)m_total);
+  ga.clip_eps = hp->ppo_clip;
+  ga.vf_coef = hp->value_loss_weight;
+  ga.ent_coef = hp->entropy_beta;
+  ga.slabs = h->slabs;
+  ga.slab_stride = h->slab_stride;
+  ga.p_total = h->layout.total;
+  int G = grad_grid(m);
+  if (G > h->G) G = h->G;
+  DPPO_TRY(launch_grad(h->sh, h->po, ga, G, s));
+  DPPO_TRY(launch_slab_reduce(h->slabs, G, h->slab_stride, h->layout.total, h->grad, nullptr,
+                              ga.inv_m, h->po.ls, d.continuous ? d.act_dim : 0, hp->entropy_beta,
+                              (d.continuous && h->rank == 0) ? 1 : 0, s));
+  DPPO_TRY(allreduce(h, h->grad, (size_t)h->layout.total + 8, ncclFloat32, s));
+  return DPPO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dppo_version(void) { return "libdppo 0.1.0 (gfx950)"; }
+
+const char* dppo_last_error(void) { return g_err; }
+
+int dppo_param_layout(const dppo_dims* dims, dppo_layout* out) {
+  DPPO_TRY(validate_dims(dims));
+  if (!out) {
+    set_error("out is NULL");
+    return DPPO_EINVAL;
+  }
+  return build_layout(dims, out);
+}
+
+int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
+  DPPO_TRY(validate_dims(dims));
+  if (!out) {
+    set_error("out is NULL");
+    return DPPO_EINVAL;
+  }
+  *out = nullptr;
+  DPPO_HIP_CHECK(hipSetDevice(device));
+  dppo_handle* h = new dppo_handle();
+  h->device = device;
+  h->dims = *dims;
+  build_layout(dims, &h->layout);
+  h->po = offsets_from_layout(*dims, h->layout);
+  h->B = (int64_t)dims->rollout_steps * dims->num_envs;
+  h->mb = (int32_t)(h->B / dims->num_minibatches);
+  h->rank = dims->rank;
+  h->nranks = dims->world_size;
+  const int D8 = (dims->obs_dim + 7) / 8 * 8;
+  h->sh.D = dims->obs_dim;
+  h->sh.D8 = D8;
+  h->sh.A = dims->act_dim;
+  h->sh.continuous = dims->continuous;
+  h->sh.R = D8 + 4 + (dims->continuous ? (dims->act_dim + 3) / 4 * 4 : 0);
+  h->mlp_ok = dims->hidden == 64 && dims->obs_dim <= 32 && dims->act_dim <= 16 &&
+              mlp_lds_bytes_grad(h->sh) <= 160 * 1024 &&
+              (size_t)(h->layout.total + 8) * 4 <= 160 * 1024;
+  h->G = grad_grid(h->mb > 0 ? h->mb : 1);
+  h->slab_stride = round_up(h->layout.total + 8, 64);
+  const int64_t E = dims->num_epochs, M = dims->num_minibatches;
+  h->trace_rows = (int32_t)(E * M);
+  int rc = DPPO_OK;
+  auto chk = [&](int r) {
+    if (rc == DPPO_OK && r != DPPO_OK) rc = r;
+  };
+  chk(dalloc(&h->logp, h->B));
+  chk(dalloc(&h->values, h->B));
+  chk(dalloc(&h->next_values, h->B));
+  chk(dalloc(&h->adv, h->B));
+  chk(dalloc(&h->ret, h->B));
+  chk(dalloc(&h->adv_n, h->B));
+  chk(dalloc(&h->rec, h->B * h->sh.R));
+  chk(dalloc(&h->slabs, (int64_t)h->G * h->slab_stride));
+  chk(dalloc(&h->grad, h->slab_stride));
+  chk(dalloc(&h->trace, E * M * DPPO_TRACE_FIELDS));
+  chk(dalloc(&h->mean_std, 4));
+  chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
+  chk(dalloc(&h->dsum, 4));
+  chk(dalloc(&h->perms_dev, E * h->B));
+  if (rc == DPPO_OK) {
+    hipError_t e = hipHostMalloc((void**)&h->perms_pinned, (size_t)(E * h->B) * sizeof(int32_t),
+                                 hipHostMallocDefault);
+    if (e != hipSuccess) {
+      set_error("hipHostMalloc failed: %s", hipGetErrorString(e));
+      rc = DPPO_ENOMEM;
+    }
+  }
+  if (rc == DPPO_OK && hipEventCreateWithFlags(&h->perm_copy_done, hipEventDisableTiming) !=
+                           hipSuccess) {
+    set_error("hipEventCreate failed");
+    rc = DPPO_EHIP;
+  }
+  if (rc == DPPO_OK) {
+    (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
+    (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
+  }
+  if (rc != DPPO_OK) {
+    dppo_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return DPPO_OK;
+}
+
+void dppo_destroy(dppo_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  if (h->comm) ncclCommDestroy(h->comm);
+  (void)hipFree(h->logp);
+  (void)hipFree(h->values);
+  (void)hipFree(h->next_values);
+  (void)hipFree(h->adv);
+  (void)hipFree(h->ret);
+  (void)hipFree(h->adv_n);
+  (void)hipFree(h->rec);
+  (void)hipFree(h->slabs);
+  (void)hipFree(h->grad);
+  (void)hipFree(h->trace);
+  (void)hipFree(h->mean_std);
+  (void)hipFree(h->partials);
+  (void)hipFree(h->dsum);
+  (void)hipFree(h->perms_dev);
+  if (h->perms_pinned) (void)hipHostFree(h->perms_pinned);
+  if (h->perm_copy_done) (void)hipEventDestroy(h->perm_copy_done);
+  delete h;
+}
+
+int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, const uint8_t* trunc,
+                 const float* values, const float* next_values, float* adv, float* returns,
+                 float gamma, float gae_lambda, void* stream) {
+  if (!h || !rewards || !term || !trunc || !values || !next_values || !adv || !returns) {
+    set_error("null argument to dppo_gae_f32");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  return launch_gae(rewards, term, trunc, values, next_values, adv, returns, h->partials,
+                    h->dims.rollout_steps, h->dims.num_envs, gamma, gae_lambda, S(stream),
+                    &h->n_partials);
+}
+
+int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream) {
+  if (!h || !mean_std) {
+    set_error("null argument to dppo_adv_stats");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, S(stream)));
+  DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, S(stream)));
+  const double n = (double)h->B * (double)(h->comm ? h->nranks : 1);
+  return launch_stats_finalize(h->dsum, n, mean_std, S(stream));
+}
+
+int dppo_adv_normalize_f32(float* adv, const float* mean_std, int64_t n, void* stream) {
+  if (!adv || !mean_std || n < 0) {
+    set_error("invalid argument to dppo_adv_normalize_f32");
+    return DPPO_EINVAL;
+  }
+  return launch_adv_normalize(adv, mean_std, n, S(stream));
+}
+
+int dppo_old_policy_f32(dppo_handle* h, const float* params, const float* obs, const void* actions,
+                        const float* next_obs, float* log_probs, float* values, float* next_values,
+                        int64_t n, void* stream) {
+  if (!h || !params || !obs || !actions || !next_obs || !log_probs || !values || !next_values ||
+      n < 0) {
+    set_error("invalid argument to dppo_old_policy_f32");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(require_mlp(h));
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  return launch_eval(h->sh, h->po, params, obs, actions, next_obs, log_probs, values,
+                     next_values, n, S(stream));
+}
+
+int dppo_prepare_f32(dppo_handle* h, const dppo_rollout* rollout, const float* params,
+                     const dppo_hparams* hp, const dppo_learn_outputs* outputs, void* stream) {
+  if (!h) {
+    set_error("null handle");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  return prepare(h, rollout, params, hp, outputs, S(stream));
+}
+
+int dppo_minibatch_grad_f32(dppo_handle* h, const float* params, const int32_t* idx, int32_t m,
+                            int32_t m_total, const dppo_hparams* hp, float* grad, float* loss4,
+                            void* stream) {
+  if (!h || !params || !idx || !hp || !grad || m < 0 || m_total <= 0) {
+    set_error("invalid argument to dppo_minibatch_grad_f32");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(require_mlp(h));
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t s = S(stream);
+  DPPO_TRY(minibatch_grad(h, params, idx, m, m_total, hp, s));
+  DPPO_HIP_CHECK(hipMemcpyAsync(grad, h->grad, (size_t)h->layout.total * sizeof(float),
+                                hipMemcpyDeviceToDevice, s));
+  if (loss4) {
+    // {loss, loss_policy, loss_value, entropy} from the summed per-sample terms (host output)
+    float tmp[8];
+    DPPO_HIP_CHECK(hipMemcpyAsync(tmp, h->grad + h->layout.total, 8 * sizeof(float),
+                                  hipMemcpyDeviceToHost, s));
+    DPPO_HIP_CHECK(hipStreamSynchronize(s));
+    const float inv = (float)(1.0 / (double)m_total);
+    const float lpi = tmp[0] * inv, lv = tmp[1] * inv, ent = tmp[2] * inv;
+    loss4[0] = lpi + hp->value_loss_weight * lv - hp->entropy_beta * ent;
+    loss4[1] = lpi;
+    loss4[2] = lv;
+    loss4[3] = ent;
+  }
+  return DPPO_OK;
+}
+
+int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v, int64_t n,
+                       float max_norm, double lr, float beta1, float beta2, float eps, int64_t step,
+                       float* out_norm, void* stream) {
+  if (!params || !grad || !adam_m || !adam_v || n < 0 || step < 1) {
+    set_error("invalid argument to dppo_clip_adam_f32");
+    return DPPO_EINVAL;
+  }
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const double step_size = lr / bc1;
+  const double bc2_sqrt = std::pow(bc2, 0.5);
+  return launch_clip_adam(params, grad, adam_m, adam_v, n, max_norm, (float)lr,
+                          (float)(-step_size), (float)bc2_sqrt, beta1, beta2, eps, out_norm,
+                          S(stream));
+}
+
+int dppo_learn_f32(dppo_handle* h, const dppo_rollout* rollout, float* params, float* adam_m,
+                   float* adam_v, const dppo_hparams* hp, const int32_t* host_perms,
+                   const dppo_learn_outputs* outputs, void* stream) {
+  if (!h || !params || !adam_m || !adam_v || !hp || !host_perms) {
+    set_error("null argument to dppo_learn_f32");
+    return DPPO_EINVAL;
+  }
+  const dppo_dims& d = h->dims;
+  if (h->B % d.num_minibatches != 0) {
+    // the reference's perms.reshape(E, M, B // M) raises ValueError (ppo.py:255)
+    set_error("cannot reshape array of size %lld into shape (%d,%d,%lld)",
+              (long long)(h->B * d.num_epochs), d.num_epochs, d.num_minibatches,
+              (long long)(h->B / d.num_minibatches));
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t s = S(stream);
+  DPPO_TRY(prepare(h, rollout, params, hp, outputs, s));
+  // permutations: host -> pinned staging -> device, stream-ordered (ppo.py:252-255)
+  const int64_t E = d.num_epochs, M = d.num_minibatches;
+  const size_t pbytes = (size_t)(E * h->B) * sizeof(int32_t);
+  if (host_perms != h->perms_pinned) {
+    if (h->perm_copy_pending) DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done));
+    std::memcpy(h->perms_pinned, host_perms, pbytes);
+  }
+  DPPO_HIP_CHECK(hipMemcpyAsync(h->perms_dev, h->perms_pinned, pbytes, hipMemcpyHostToDevice, s));
+  DPPO_HIP_CHECK(hipEventRecord(h->perm_copy_done, s));
+  h->perm_copy_pending = true;
+  // (6) E x M dependent optimizer steps (ppo.py:258-285)
+  const int32_t mb = h->mb;
+  const int32_t m_total = mb * (h->comm ? h->nranks : 1);
+  const float inv_m = (float)(1.0 / (double)m_total);
+  for (int64_t e = 0; e < E; ++e) {
+    for (int64_t j = 0; j < M; ++j) {
+      const int64_t k = e * M + j;
+      const int32_t* idx = h->perms_dev + e * h->B + j * mb;
+      DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
+      const double step = (double)(hp->adam_step + k + 1);
+      const double bc1 = 1.0 - std::pow((double)hp->adam_beta1, step);
+      const double bc2 = 1.0 - std::pow((double)hp->adam_beta2, step);
+      const double step_size = hp->lr / bc1;
+      const double bc2_sqrt = std::pow(bc2, 0.5);
+      DPPO_TRY(launch_clip_adam_traced(params, h->grad, adam_m, adam_v, h->layout.total,
+                                       hp->grad_norm_clip, (float)hp->lr, (float)(-step_size),
+                                       (float)bc2_sqrt, hp->adam_beta1, hp->adam_beta2,
+                                       hp->adam_eps, nullptr, h->trace + k * DPPO_TRACE_FIELDS,
+                                       inv_m, hp->value_loss_weight, hp->entropy_beta, s));
+    }
+  }
+  h->last_stream = s;
+  return DPPO_OK;
+}
+
+int dppo_perm_buffer(dppo_handle* h, int32_t** out) {
+  if (!h || !out) {
+    set_error("null argument to dppo_perm_buffer");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  if (h->perm_copy_pending) {
+    DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done));
+    h->perm_copy_pending = false;
+  }
+  *out = h->perms_pinned;
+  return DPPO_OK;
+}
+
+int dppo_get_trace(dppo_handle* h, float* host_out, int32_t rows) {
+  if (!h || !host_out || rows < 0 || rows > h->trace_rows) {
+    set_error("invalid argument to dppo_get_trace");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  DPPO_HIP_CHECK(hipStreamSynchronize(h->last_stream));
+  DPPO_HIP_CHECK(hipMemcpy(host_out, h->trace, (size_t)rows * DPPO_TRACE_FIELDS * sizeof(float),
+                           hipMemcpyDeviceToHost));
+  return DPPO_OK;
+}
+
+int dppo_comm_unique_id(char* out128) {
+  if (!out128) {
+    set_error("null argument");
+    return DPPO_EINVAL;
+  }
+  ncclUniqueId id;
+  DPPO_NCCL_CHECK(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out128, &id, 128);
+  return DPPO_OK;
+}
+
+int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128) {
+  if (!h || !id128 || nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("invalid argument to dppo_comm_init");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  ncclUniqueId id;
+  std::memcpy(&id, id128, 128);
+  ncclComm_t c;
+  DPPO_NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+  h->comm = c;
+  h->nranks = nranks;
+  h->rank = rank;
+  return DPPO_OK;
+}
+
+}  // extern "C"

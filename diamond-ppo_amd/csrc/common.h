@@ -1,0 +1,97 @@
+// Device-side common definitions for the gfx950 kernels of libdppo.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dppo_host.h"
+
+#define DPPO_HIP_CHECK(expr)                                                              \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      ::dppo::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,  \
+                        __LINE__);                                                        \
+      return DPPO_EHIP;                                                                   \
+    }                                                                                     \
+  } while (0)
+
+#define DPPO_LAUNCH_CHECK()                                                               \
+  do {                                                                                    \
+    hipError_t e_ = hipGetLastError();                                                    \
+    if (e_ != hipSuccess) {                                                               \
+      ::dppo::set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(e_),        \
+                        __FILE__, __LINE__);                                              \
+      return DPPO_EHIP;                                                                   \
+    }                                                                                     \
+  } while (0)
+
+namespace dppo {
+
+constexpr int kWave = 64;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Launchers implemented in the .hip files (all stream-ordered, no host sync).
+int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
+               const float* nv, float* adv, float* ret, double* partials, int T, int N,
+               float gamma, float gae_lambda, hipStream_t s, int* n_partials);
+int launch_stats_reduce(const double* partials, int n_partials, double* dsum, hipStream_t s);
+int launch_stats_finalize(const double* dsum, double n_total, float* mean_std, hipStream_t s);
+int launch_adv_normalize(float* adv, const float* mean_std, int64_t n, hipStream_t s);
+
+struct PackArgs {
+  const float* obs;       // [B][D]
+  const void* actions;    // int32 [B] or float [B][A]
+  const float* logp;      // [B]
+  const float* adv;       // [B] raw advantages
+  const float* ret;       // [B]
+  const double* dsum;     // {sum, sumsq} of raw advantages (global), or null if no norm
+  double n_total;         // global sample count for the statistics
+  int advantage_norm;
+  float* adv_out;         // optional [B]: the (normalised) advantages handed to the update
+  float* rec;             // [B][R]
+  int64_t B;
+  int D, D8, A, R, continuous;
+};
+int launch_pack(const PackArgs& a, hipStream_t s);
+
+// Default actor-critic MLP (hidden 64) kernels: mlp.hip.
+struct MlpShape {
+  int D, D8, A, continuous, R;  // R = record stride (floats)
+};
+size_t mlp_lds_bytes_grad(const MlpShape& sh);
+size_t mlp_lds_bytes_eval(const MlpShape& sh);
+int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
+                const void* actions, const float* next_obs, float* logp, float* values,
+                float* next_values, int64_t n, hipStream_t s);
+struct GradArgs {
+  const float* params;
+  const float* rec;
+  const int32_t* idx;  // minibatch sample indices (local)
+  int32_t m;           // samples in this minibatch on this rank
+  float inv_m;         // 1 / global minibatch size
+  float clip_eps, vf_coef, ent_coef;
+  float* slabs;        // [G][slab_stride]
+  int64_t slab_stride; // floats per slab (param total + 8 loss slots, rounded)
+  int64_t p_total;
+};
+int grad_grid(int32_t m);
+int launch_grad(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
+                hipStream_t s);
+
+// Optimiser kernels: optim.hip.
+int launch_slab_reduce(const float* slabs, int G, int64_t slab_stride, int64_t p_total,
+                       float* grad, float* loss4, float inv_m, int64_t ls_off, int ls_n,
+                       float ent_coef, int add_entropy_const, hipStream_t s);
+int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int64_t n,
+                            float max_norm, float lr, float neg_step_size, float bc2_sqrt,
+                            float beta1, float beta2, float eps, float* out_norm, float* trace,
+                            float inv_m, float vf, float ent, hipStream_t s);
+int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, float max_norm,
+                     float lr, float neg_step_size, float bc2_sqrt, float beta1, float beta2,
+                     float eps, float* out_norm, hipStream_t s);
+
+}  // namespace dppo

@@ -1,0 +1,218 @@
+"""ctypes binding of libdppo (the gfx950 C ABI declared in include/dppo.h).
+
+This is the product path: there is no CPU fallback.  If the shared library is missing or no
+HIP device is present, the loaders raise instead of computing anything on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DPPO_LIB", os.path.join(_HERE, "libdppo.so"))
+
+DPPO_OK = 0
+DPPO_EINVAL = -1
+DPPO_EHIP = -2
+DPPO_EUNSUPPORTED = -3
+DPPO_ENOMEM = -4
+DPPO_ECOMM = -5
+MAX_TENSORS = 16
+TRACE_FIELDS = 5
+
+EXPORTED = [
+    "dppo_version", "dppo_last_error", "dppo_param_layout", "dppo_create", "dppo_destroy",
+    "dppo_gae_f32", "dppo_adv_stats", "dppo_adv_normalize_f32", "dppo_old_policy_f32",
+    "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
+    "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
+    "dppo_comm_init",
+]
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("rollout_steps", ctypes.c_int32), ("num_envs", ctypes.c_int32),
+                ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32),
+                ("continuous", ctypes.c_int32), ("hidden", ctypes.c_int32),
+                ("num_epochs", ctypes.c_int32), ("num_minibatches", ctypes.c_int32),
+                ("world_size", ctypes.c_int32), ("rank", ctypes.c_int32)]
+
+
+class HParams(ctypes.Structure):
+    _fields_ = [("gamma", ctypes.c_float), ("gae_lambda", ctypes.c_float),
+                ("ppo_clip", ctypes.c_float), ("value_loss_weight", ctypes.c_float),
+                ("entropy_beta", ctypes.c_float), ("grad_norm_clip", ctypes.c_float),
+                ("adam_beta1", ctypes.c_float), ("adam_beta2", ctypes.c_float),
+                ("adam_eps", ctypes.c_float), ("advantage_norm", ctypes.c_int32),
+                ("lr", ctypes.c_double), ("adam_step", ctypes.c_int64)]
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [("total", ctypes.c_int64), ("n_real", ctypes.c_int64),
+                ("count", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("offset", ctypes.c_int64 * MAX_TENSORS), ("numel", ctypes.c_int64 * MAX_TENSORS),
+                ("rows", ctypes.c_int32 * MAX_TENSORS), ("cols", ctypes.c_int32 * MAX_TENSORS)]
+
+
+class Rollout(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("next_obs", ctypes.c_void_p),
+                ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("term", ctypes.c_void_p), ("trunc", ctypes.c_void_p)]
+
+
+class LearnOutputs(ctypes.Structure):
+    _fields_ = [("log_probs", ctypes.c_void_p), ("values", ctypes.c_void_p),
+                ("next_values", ctypes.c_void_p), ("advantages", ctypes.c_void_p),
+                ("returns", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load():
+    """Load libdppo.so (raises ImportError if it was not built: run __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libdppo.so not found at {LIB_PATH}; build it with "
+                          f"`make -C diamond-ppo_amd` (hipcc --offload-arch=gfx950)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, f32, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double
+    P = ctypes.POINTER
+    sig = {
+        "dppo_version": (ctypes.c_char_p, []),
+        "dppo_last_error": (ctypes.c_char_p, []),
+        "dppo_param_layout": (ctypes.c_int, [P(Dims), P(Layout)]),
+        "dppo_create": (ctypes.c_int, [ctypes.c_int, P(Dims), P(vp)]),
+        "dppo_destroy": (None, [vp]),
+        "dppo_gae_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
+        "dppo_adv_stats": (ctypes.c_int, [vp, vp, vp]),
+        "dppo_adv_normalize_f32": (ctypes.c_int, [vp, vp, i64, vp]),
+        "dppo_old_policy_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "dppo_learn_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,
+                                          P(LearnOutputs), vp]),
+        "dppo_minibatch_grad_f32": (ctypes.c_int, [vp, vp, vp, i32, i32, P(HParams), vp, vp, vp]),
+        "dppo_prepare_f32": (ctypes.c_int, [vp, P(Rollout), vp, P(HParams), P(LearnOutputs), vp]),
+        "dppo_clip_adam_f32": (ctypes.c_int, [vp, vp, vp, vp, i64, f32, f64, f32, f32, f32, i64,
+                                              vp, vp]),
+        "dppo_perm_buffer": (ctypes.c_int, [vp, P(vp)]),
+        "dppo_get_trace": (ctypes.c_int, [vp, vp, i32]),
+        "dppo_perm_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
+        "dppo_comm_unique_id": (ctypes.c_int, [vp]),
+        "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = ""):
+    """Map libdppo status codes onto the exception types the reference raises."""
+    if rc == DPPO_OK:
+        return
+    msg = load().dppo_last_error().decode(errors="replace")
+    text = f"{what}: {msg}" if what else msg
+    if rc == DPPO_EINVAL:
+        raise ValueError(text)
+    if rc == DPPO_EUNSUPPORTED:
+        raise NotImplementedError(text)
+    if rc == DPPO_ENOMEM:
+        raise MemoryError(text)
+    raise NativeError(f"libdppo error {rc}: {text}")
+
+
+def ptr(t) -> int:
+    """Raw device/host address of a torch tensor or numpy array (None -> 0)."""
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def param_layout(dims: Dims) -> Layout:
+    L = Layout()
+    check(load().dppo_param_layout(ctypes.byref(dims), ctypes.byref(L)), "dppo_param_layout")
+    return L
+
+
+def perm_numpy(key: np.ndarray, pos: int, n: int, count: int, out: np.ndarray | int) -> int:
+    """NumPy-legacy-exact permutations (host C++).  ``key`` (uint32[624]) is advanced in place;
+    returns the new ``pos``.  ``out`` is an int32 array of count*n or a raw host address."""
+    assert key.dtype == np.uint32 and key.size == 624 and key.flags.c_contiguous
+    p = ctypes.c_int32(int(pos))
+    dst = out if isinstance(out, int) else out.ctypes.data
+    if not isinstance(out, int):
+        assert out.dtype == np.int32 and out.size >= n * count and out.flags.c_contiguous
+    check(load().dppo_perm_numpy(key.ctypes.data, ctypes.byref(p), int(n), int(count), dst),
+          "dppo_perm_numpy")
+    return int(p.value)
+
+
+def numpy_rng_permutations(n: int, count: int, out, rng=None):
+    """Draw ``count`` permutations of range(n) exactly as ``count`` calls of
+    ``rng.permutation(n)`` would (rng = the global legacy NumPy RNG by default, reference
+    ppo.py:254), leaving the RNG in the same final state."""
+    st = (np.random.get_state() if rng is None else rng.get_state())
+    if st[0] != "MT19937":
+        raise ValueError("only the legacy MT19937 RandomState is supported")
+    key = np.array(st[1], dtype=np.uint32, copy=True)
+    pos = perm_numpy(key, int(st[2]), n, count, out)
+    new = (st[0], key, pos, st[3], st[4])
+    if rng is None:
+        np.random.set_state(new)
+    else:
+        rng.set_state(new)
+
+
+class Handle:
+    """Owns one dppo_handle (device workspace sized for one rollout shape)."""
+
+    def __init__(self, device_index: int, dims: Dims):
+        self.lib = load()
+        self.dims = dims
+        h = ctypes.c_void_p()
+        check(self.lib.dppo_create(int(device_index), ctypes.byref(dims), ctypes.byref(h)),
+              "dppo_create")
+        self.h = h
+        self.layout = param_layout(dims)
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.lib.dppo_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def perm_buffer(self) -> int:
+        p = ctypes.c_void_p()
+        check(self.lib.dppo_perm_buffer(self.h, ctypes.byref(p)), "dppo_perm_buffer")
+        return p.value
+
+    def trace(self, rows: int) -> np.ndarray:
+        out = np.zeros((rows, TRACE_FIELDS), np.float32)
+        check(self.lib.dppo_get_trace(self.h, out.ctypes.data, int(rows)), "dppo_get_trace")
+        return out
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = ctypes.create_string_buffer(uid, 128)
+        check(self.lib.dppo_comm_init(self.h, int(nranks), int(rank), buf), "dppo_comm_init")
+
+
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    check(load().dppo_comm_unique_id(buf), "dppo_comm_unique_id")
+    return buf.raw

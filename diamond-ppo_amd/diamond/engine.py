@@ -1,0 +1,325 @@
+"""The learn() driver shared by PPO and ContinuousPPO.
+
+Host side of the hot path (reference ``diamond/ppo.py:224-287``): it owns the flat parameter /
+Adam buffers the gfx950 kernels update in place, keeps the reference's ``nn.Module`` and
+``torch.optim.Adam`` objects as live views of those buffers (so ``state_dict()``, checkpoints and
+``LinearLR`` behave exactly as in the reference), draws the minibatch permutations from the global
+NumPy RNG bit-exactly, and issues ONE native call per learn().
+
+Two paths, chosen once per agent:
+
+* **fused** -- default network at supported sizes (hidden 64, obs_dim <= 32, actions <= 16):
+  everything in ``dppo_learn_f32`` (old-policy eval, GAE, normalisation, E x M fused
+  minibatch steps with clip + Adam, RCCL all-reduces when sharded).
+* **generic** -- any other ``network_cls`` (reference readme.md:89-111): the network's own
+  methods run forward/backward under torch autograd on the GPU; GAE, advantage statistics and
+  normalisation, and clip + Adam run in the HIP kernels (SURVEY.md §7.2 hard part 7).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def require_gpu(cfg_device_index: int = 0) -> torch.device:
+    """The product path runs on the MI355X only; fail loudly otherwise (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("diamond (MI355X build) requires a HIP GPU; none is visible. "
+                           "The reference's CPU path is not part of this package.")
+    N.load()
+    idx = cfg_device_index
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        import os
+        idx = int(os.environ.get("LOCAL_RANK", idx))
+    return torch.device("cuda", idx)
+
+
+def dist_world():
+    d = torch.distributed
+    if d.is_available() and d.is_initialized():
+        return d.get_world_size(), d.get_rank()
+    return 1, 0
+
+
+# ---------------------------------------------------------------------------------------------
+class FlatParams:
+    """Re-home every parameter of ``module`` into one flat device buffer at the given offsets
+    (tensors in ``named_parameters()`` order).  Parameters become views, so the module, its
+    ``state_dict()`` and the optimizer all see the values the kernels write."""
+
+    def __init__(self, module: torch.nn.Module, device, offsets=None, total=None):
+        params = list(module.parameters())
+        if offsets is None:
+            offsets, off = [], 0
+            for p in params:
+                offsets.append(off)
+                off = (off + p.numel() + 15) // 16 * 16
+            total = off
+        self.offsets = list(offsets)
+        self.total = int(total)
+        self.shapes = [tuple(p.shape) for p in params]
+        self.numels = [p.numel() for p in params]
+        self.flat = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(self.total + 8, dtype=torch.float32, device=device)
+        with torch.no_grad():
+            for p, o, n, s in zip(params, self.offsets, self.numels, self.shapes):
+                self.flat[o:o + n].copy_(p.detach().reshape(-1).to(device))
+                p.data = self.flat[o:o + n].view(s)
+        self.params = params
+
+    def views(self, buf):
+        return [buf[o:o + n].view(s) for o, n, s in zip(self.offsets, self.numels, self.shapes)]
+
+    def bind_grads(self):
+        """Make p.grad views of the flat grad buffer (autograd accumulates into them in place)."""
+        for p, g in zip(self.params, self.views(self.grad)):
+            p.grad = g
+
+
+def bind_adam_state(optimizer: torch.optim.Adam, flat: FlatParams):
+    """Initialise torch Adam's per-parameter state as views of flat exp_avg / exp_avg_sq buffers
+    (the layout torch would create lazily at the first step: optim/adam.py _init_group)."""
+    m = torch.zeros_like(flat.flat)
+    v = torch.zeros_like(flat.flat)
+    for p, mv, vv in zip(flat.params, flat.views(m), flat.views(v)):
+        optimizer.state[p] = {"step": torch.tensor(0.0, dtype=torch.float32),
+                              "exp_avg": mv, "exp_avg_sq": vv}
+    return m, v
+
+
+def adam_step_count(optimizer, flat: FlatParams) -> int:
+    st = optimizer.state.get(flat.params[0])
+    return int(st["step"].item()) if st and "step" in st else 0
+
+
+def advance_adam_steps(optimizer, flat: FlatParams, k: int):
+    for p in flat.params:
+        optimizer.state[p]["step"] += float(k)
+
+
+def rebind_after_load(optimizer, flat: FlatParams, m, v):
+    """After optimizer.load_state_dict (which replaces state tensors), copy values back into the
+    flat buffers and restore the views."""
+    with torch.no_grad():
+        for p, mv, vv in zip(flat.params, flat.views(m), flat.views(v)):
+            st = optimizer.state[p]
+            if "exp_avg" in st and st["exp_avg"].data_ptr() != mv.data_ptr():
+                mv.copy_(st["exp_avg"])
+                vv.copy_(st["exp_avg_sq"])
+                st["exp_avg"], st["exp_avg_sq"] = mv, vv
+            if not isinstance(st.get("step"), torch.Tensor):
+                st["step"] = torch.tensor(float(st.get("step", 0.0)), dtype=torch.float32)
+
+
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class DeviceRollout:
+    """SoA rollout buffer resident in HBM (layouts in include/dppo.h)."""
+    obs: torch.Tensor          # float32 [T, N, D]
+    next_obs: torch.Tensor     # float32 [T, N, D]
+    actions: torch.Tensor      # int32 [T, N] or float32 [T, N, A]
+    rewards: torch.Tensor      # float32 [T, N]
+    term: torch.Tensor         # uint8 [T, N]
+    trunc: torch.Tensor        # uint8 [T, N]
+
+    def check(self, T, N, D, A, continuous):
+        def need(t, shape, dtype, name):
+            if tuple(t.shape) != shape or t.dtype != dtype or not t.is_contiguous() or not t.is_cuda:
+                raise ValueError(f"{name}: expected contiguous {dtype} {shape} on GPU, got "
+                                 f"{t.dtype} {tuple(t.shape)} on {t.device}")
+        need(self.obs, (T, N, D), torch.float32, "obs")
+        need(self.next_obs, (T, N, D), torch.float32, "next_obs")
+        if continuous:
+            need(self.actions, (T, N, A), torch.float32, "actions")
+        else:
+            need(self.actions, (T, N), torch.int32, "actions")
+        need(self.rewards, (T, N), torch.float32, "rewards")
+        need(self.term, (T, N), torch.uint8, "term")
+        need(self.trunc, (T, N), torch.uint8, "trunc")
+
+    def as_struct(self) -> N.Rollout:
+        return N.Rollout(self.obs.data_ptr(), self.next_obs.data_ptr(), self.actions.data_ptr(),
+                         self.rewards.data_ptr(), self.term.data_ptr(), self.trunc.data_ptr())
+
+
+def stage_experience(experience, device, continuous) -> DeviceRollout:
+    """Stack the rollout lists (ppo.py:226-232) into SoA device tensors.  Host bytes go through
+    pinned memory so the H2D copies are DMA transfers."""
+    obs, next_obs, actions, rewards, terms, truncs = zip(*experience)
+
+    def up(x, dtype):
+        a = np.ascontiguousarray(np.asarray(x), dtype=dtype)
+        return torch.from_numpy(a).pin_memory().to(device, non_blocking=True)
+
+    act_dtype = np.float32 if continuous else np.int32
+    return DeviceRollout(up(obs, np.float32), up(next_obs, np.float32), up(actions, act_dtype),
+                         up(rewards, np.float32), up(terms, np.uint8), up(truncs, np.uint8))
+
+
+def hparams(cfg, lr: float, adam_step: int, betas=(0.9, 0.999)) -> N.HParams:
+    return N.HParams(gamma=cfg.gamma, gae_lambda=cfg.gae_lambda, ppo_clip=cfg.ppo_clip,
+                     value_loss_weight=cfg.value_loss_weight, entropy_beta=cfg.entropy_beta,
+                     grad_norm_clip=cfg.grad_norm_clip, adam_beta1=betas[0], adam_beta2=betas[1],
+                     adam_eps=cfg.adam_eps, advantage_norm=int(bool(cfg.advantage_norm)),
+                     lr=float(lr), adam_step=int(adam_step))
+
+
+# ---------------------------------------------------------------------------------------------
+class NativeLearner:
+    """Binds one agent (network + Adam) to a libdppo handle for its rollout shape."""
+
+    def __init__(self, network, optimizer, cfg, obs_dim, act_dim, continuous, device,
+                 network_is_default: bool):
+        self.cfg = cfg
+        self.device = device
+        self.continuous = bool(continuous)
+        self.world, self.rank = dist_world()
+        self.T, self.N = cfg.rollout_steps, cfg.num_envs
+        self.D, self.A = obs_dim, act_dim
+        self.dims = N.Dims(rollout_steps=self.T, num_envs=self.N, obs_dim=obs_dim,
+                           act_dim=act_dim, continuous=int(continuous),
+                           hidden=int(cfg.network_hidden_dim), num_epochs=cfg.num_epochs,
+                           num_minibatches=cfg.num_minibatches, world_size=self.world,
+                           rank=self.rank)
+        self.handle = N.Handle(device.index or 0, self.dims)
+        L = self.handle.layout
+        names = [n for n, _ in network.named_parameters()]
+        shapes_ok = network_is_default and L.count == len(names) and all(
+            tuple(p.shape) in ((L.rows[i], L.cols[i]), (L.rows[i],)) for i, (_, p) in
+            enumerate(network.named_parameters()))
+        self.fused = bool(shapes_ok and cfg.network_hidden_dim == 64 and obs_dim <= 32
+                          and act_dim <= 16)
+        if self.fused:
+            self.flat = FlatParams(network, device, [L.offset[i] for i in range(L.count)], L.total)
+        else:
+            self.flat = FlatParams(network, device)
+            self.flat.bind_grads()
+        self.m, self.v = bind_adam_state(optimizer, self.flat)
+        self.optimizer = optimizer
+        self.network = network
+        if self.world > 1:
+            self._init_comm()
+        self.last_trace = None
+
+    def _init_comm(self):
+        d = torch.distributed
+        obj = [N.comm_unique_id() if self.rank == 0 else None]
+        d.broadcast_object_list(obj, src=0)
+        self.handle.comm_init(self.world, self.rank, obj[0])
+        # replicate rank 0's initial parameters (identical seeds make this a no-op in practice)
+        if d.get_backend() == "nccl":
+            d.broadcast(self.flat.flat, src=0)
+        else:
+            cpu = self.flat.flat.cpu()
+            d.broadcast(cpu, src=0)
+            self.flat.flat.copy_(cpu)
+
+    # -----------------------------------------------------------------------------------------
+    def draw_permutations(self, out_addr: int):
+        """np.random.permutation(B) for each epoch (ppo.py:252-254), bit-exact, written into the
+        pinned staging buffer at ``out_addr`` (one contiguous [E][B] int32 block)."""
+        B = self.T * self.N
+        N.numpy_rng_permutations(B, self.cfg.num_epochs, out_addr)
+
+    def learn(self, ro: DeviceRollout, lr: float, outputs: N.LearnOutputs | None = None):
+        cfg = self.cfg
+        B = self.T * self.N
+        if B % cfg.num_minibatches != 0:
+            # reference: perms.reshape(E, M, B // M) raises (ppo.py:255)
+            raise ValueError(f"cannot reshape array of size {B * cfg.num_epochs} into shape "
+                             f"({cfg.num_epochs},{cfg.num_minibatches},{B // cfg.num_minibatches})")
+        ro.check(self.T, self.N, self.D, self.A, self.continuous)
+        step0 = adam_step_count(self.optimizer, self.flat)
+        if self.fused:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            pinned = self.handle.perm_buffer()
+            self.draw_permutations(pinned)
+            hp = hparams(cfg, lr, step0)
+            N.check(self.handle.lib.dppo_learn_f32(
+                self.handle.h, ctypes.byref(ro.as_struct()), self.flat.flat.data_ptr(),
+                self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
+                ctypes.byref(outputs) if outputs is not None else None, stream), "dppo_learn_f32")
+        else:
+            self._learn_generic(ro, lr, step0)
+        advance_adam_steps(self.optimizer, self.flat, cfg.num_epochs * cfg.num_minibatches)
+
+    def trace(self) -> np.ndarray:
+        """Per optimizer step {loss, loss_policy, loss_value, entropy, grad_norm} of the last
+        fused learn() (synchronises)."""
+        return self.handle.trace(self.cfg.num_epochs * self.cfg.num_minibatches)
+
+    # -----------------------------------------------------------------------------------------
+    def _learn_generic(self, ro: DeviceRollout, lr: float, step0: int):
+        """Custom network_cls: torch autograd for the network, HIP kernels for GAE,
+        normalisation and clip + Adam (reference ppo.py:224-287 step by step)."""
+        cfg, lib, h = self.cfg, self.handle.lib, self.handle.h
+        T, Nn = self.T, self.N
+        B = T * Nn
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        net = self.network
+        with torch.inference_mode():
+            if self.continuous:
+                means, log_stds, values = net.get_means_log_stds_and_values(ro.obs)
+                from .continuous_ppo import JointNormal
+                log_probs = JointNormal(loc=means, scale=log_stds.exp()).log_prob(ro.actions)
+            else:
+                logits, values = net.get_logits_and_values(ro.obs)
+                log_probs = torch.distributions.Categorical(logits=logits).log_prob(
+                    ro.actions.long())
+            next_values = net.get_values(ro.next_obs)
+        values = values.float().contiguous()
+        next_values = next_values.float().contiguous()
+        adv = torch.empty_like(values)
+        ret = torch.empty_like(values)
+        N.check(lib.dppo_gae_f32(h, ro.rewards.data_ptr(), ro.term.data_ptr(), ro.trunc.data_ptr(),
+                                 values.data_ptr(), next_values.data_ptr(), adv.data_ptr(),
+                                 ret.data_ptr(), cfg.gamma, cfg.gae_lambda, stream), "dppo_gae_f32")
+        if cfg.advantage_norm:
+            ms = torch.empty(4, dtype=torch.float32, device=self.device)
+            N.check(lib.dppo_adv_stats(h, ms.data_ptr(), stream), "dppo_adv_stats")
+            N.check(lib.dppo_adv_normalize_f32(adv.data_ptr(), ms.data_ptr(), B, stream),
+                    "dppo_adv_normalize_f32")
+        obs = ro.obs.reshape(B, *ro.obs.shape[2:])
+        acts = ro.actions.reshape(B, *ro.actions.shape[2:])
+        if not self.continuous:
+            acts = acts.long()
+        log_probs, adv, ret = log_probs.reshape(B), adv.reshape(B), ret.reshape(B)
+        mb = B // cfg.num_minibatches
+        perms = np.empty(cfg.num_epochs * B, np.int32)
+        N.numpy_rng_permutations(B, cfg.num_epochs, perms)
+        idx_all = torch.from_numpy(perms.astype(np.int64)).to(self.device).view(
+            cfg.num_epochs, cfg.num_minibatches, mb)
+        step = step0
+        for b_idx in idx_all:
+            for mb_idx in b_idx:
+                self.flat.grad.zero_()
+                if self.continuous:
+                    from .continuous_ppo import JointNormal
+                    m_, ls_, v_ = net.get_means_log_stds_and_values(obs[mb_idx])
+                    dist = JointNormal(loc=m_, scale=ls_.exp())
+                    new_v = v_
+                else:
+                    lg, new_v = net.get_logits_and_values(obs[mb_idx])
+                    dist = torch.distributions.Categorical(logits=lg)
+                new_lp = dist.log_prob(acts[mb_idx])
+                ratio = (new_lp - log_probs[mb_idx]).exp()
+                a_mb = adv[mb_idx]
+                l_pi = torch.max(-a_mb * ratio,
+                                 -a_mb * torch.clamp(ratio, 1.0 - cfg.ppo_clip, 1.0 + cfg.ppo_clip)).mean()
+                l_v = 0.5 * torch.nn.functional.mse_loss(new_v, ret[mb_idx])
+                ent = dist.entropy().mean()
+                loss = l_pi + cfg.value_loss_weight * l_v + -cfg.entropy_beta * ent
+                loss.backward()
+                if self.world > 1:
+                    torch.distributed.all_reduce(self.flat.grad)
+                    self.flat.grad.div_(self.world)
+                step += 1
+                N.check(lib.dppo_clip_adam_f32(
+                    self.flat.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
+                    self.v.data_ptr(), self.flat.total, cfg.grad_norm_clip, float(lr), 0.9, 0.999,
+                    cfg.adam_eps, step, None, stream), "dppo_clip_adam_f32")

@@ -1,0 +1,189 @@
+/*
+ * libdppo -- MI355X (gfx950) native PPO hot path: GAE + clipped-surrogate minibatch update.
+ *
+ * C ABI (plain pointers and sizes, no torch types).  Every call that touches the GPU is
+ * stream-ordered on the caller's hipStream_t (passed as void*; NULL = legacy default stream),
+ * performs no host synchronisation unless documented, and never allocates on the hot path:
+ * workspace is allocated once by dppo_create().  Handles are reentrant across handles, NOT
+ * thread-safe on one handle.  One process per GPU.
+ *
+ * The reference (Auxeno/diamond-ppo) is pure Python with no FFI; each entry point below names
+ * the reference code it replaces (file:line in diamond/).  The Python host mirror that binds
+ * this ABI is diamond-ppo_amd/diamond/_native.py (ctypes); see INTEGRATION.md.
+ *
+ * Layouts (HBM, structure-of-arrays, flat sample index i = t*N + n, reference ppo.py:246-249):
+ *   obs, next_obs  float32 [T][N][D]          rewards        float32 [T][N]
+ *   term, trunc    uint8   [T][N] (0/1)       actions        int32 [T][N] (discrete) or
+ *                                                            float32 [T][N][A] (continuous)
+ *   params, adam m/v: one flat float32 buffer each, tensors at dppo_param_layout() offsets.
+ *
+ * Status codes: 0 = OK, negative = error; dppo_last_error() describes the last failure on the
+ * calling thread.  The Python binding maps them to the reference's exception types.
+ */
+#ifndef DPPO_H_
+#define DPPO_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPPO_OK 0
+#define DPPO_EINVAL (-1)       /* invalid argument (Python: ValueError / AssertionError) */
+#define DPPO_EHIP (-2)         /* HIP runtime error (Python: RuntimeError) */
+#define DPPO_EUNSUPPORTED (-3) /* shape outside the fused kernels' support (Python: NotImplementedError) */
+#define DPPO_ENOMEM (-4)       /* workspace allocation failed (Python: MemoryError) */
+#define DPPO_ECOMM (-5)        /* RCCL failure (Python: RuntimeError) */
+
+#define DPPO_MAX_TENSORS 16
+#define DPPO_TRACE_FIELDS 5 /* per optimizer step: loss, loss_policy, loss_value, entropy, grad_norm */
+
+typedef struct dppo_handle dppo_handle;
+
+/* Shapes.  Mirrors the PPOConfig / ContinuousPPOConfig fields the hot path reads
+ * (reference ppo.py:15-37, continuous_ppo.py:15-37) plus the env-axis shard. */
+typedef struct dppo_dims {
+  int32_t rollout_steps;   /* T */
+  int32_t num_envs;        /* N: envs owned by THIS rank */
+  int32_t obs_dim;         /* D = prod(observation_space.shape)        (ppo.py:54) */
+  int32_t act_dim;         /* discrete: action_space.n; continuous: prod(action_space.shape) */
+  int32_t continuous;      /* 0 = PPO/Categorical, 1 = ContinuousPPO/JointNormal */
+  int32_t hidden;          /* network_hidden_dim (ppo.py:32,51) */
+  int32_t num_epochs;      /* ppo.py:25 */
+  int32_t num_minibatches; /* ppo.py:26 */
+  int32_t world_size;      /* ranks sharing the env axis (1 = single GPU) */
+  int32_t rank;
+} dppo_dims;
+
+/* Hyper-parameters of one learn() call (ppo.py:15-37, Adam defaults torch/optim/adam.py:39). */
+typedef struct dppo_hparams {
+  float gamma, gae_lambda, ppo_clip, value_loss_weight, entropy_beta, grad_norm_clip;
+  float adam_beta1, adam_beta2, adam_eps;
+  int32_t advantage_norm;
+  double lr;         /* current learning rate (after LinearLR, ppo.py:137-142,287) */
+  int64_t adam_step; /* optimizer steps taken before this call (torch Adam state['step']) */
+} dppo_hparams;
+
+/* Flat parameter layout, tensors in the reference's named_parameters() order
+ * (discrete: base.0.{weight,bias}, base.2.*, actor_head.0.*, actor_head.2.*, critic_head.0.*,
+ *  critic_head.2.*; continuous: actor_log_std first, then base, actor_mean_head, critic_head).
+ * Each tensor starts on a 64-byte boundary; padding floats are never read as parameters. */
+typedef struct dppo_layout {
+  int64_t total;  /* floats in the flat buffer, padding included */
+  int64_t n_real; /* real parameter count (12,995 for CartPole at hidden 64) */
+  int32_t count;  /* number of tensors */
+  int32_t pad_;
+  int64_t offset[DPPO_MAX_TENSORS];
+  int64_t numel[DPPO_MAX_TENSORS];
+  int32_t rows[DPPO_MAX_TENSORS]; /* weight [out][in]: rows=out, cols=in; bias: rows=n, cols=1 */
+  int32_t cols[DPPO_MAX_TENSORS];
+} dppo_layout;
+
+/* Device rollout buffer (caller-owned). */
+typedef struct dppo_rollout {
+  const float* obs;
+  const float* next_obs;
+  const void* actions; /* int32 [T][N] or float32 [T][N][A] */
+  const float* rewards;
+  const uint8_t* term;
+  const uint8_t* trunc;
+} dppo_rollout;
+
+/* Optional caller-owned device outputs of one learn() (NULL = keep internal).  All [T*N]. */
+typedef struct dppo_learn_outputs {
+  float* log_probs;   /* old-policy log pi(a|s)                         ppo.py:237 */
+  float* values;      /* V(s)                                           ppo.py:236 */
+  float* next_values; /* V(s')                                          ppo.py:238 */
+  float* advantages;  /* GAE, normalised if advantage_norm              ppo.py:240-243 */
+  float* returns;     /* values + raw advantages                        ppo.py:241 */
+} dppo_learn_outputs;
+
+const char* dppo_version(void);
+const char* dppo_last_error(void);
+int dppo_param_layout(const dppo_dims* dims, dppo_layout* out);
+
+/* Workspace sized for dims (rollout buffers, sample records, gradient slabs, trace). */
+int dppo_create(int device, const dppo_dims* dims, dppo_handle** out);
+void dppo_destroy(dppo_handle* h);
+
+/* GAE over the [T][N] buffers: replaces PPO.calculate_advantage (ppo.py:188-222; identical in
+ * continuous_ppo.py:200-234, recurrent_ppo.py:265-299) fused with returns = values + adv
+ * (ppo.py:241).  Bit-exact with the reference's fp32 op order.  Also records the per-tile
+ * (sum, sum of squares) partials the next call reduces. */
+int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, const uint8_t* trunc,
+                 const float* values, const float* next_values, float* adv, float* returns,
+                 float gamma, float gae_lambda, void* stream);
+
+/* Mean and unbiased std of the advantages of the last dppo_gae_f32 (ppo.py:243, reduced over
+ * all ranks when a communicator is attached); writes device float mean_std[2]. */
+int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream);
+
+/* adv = (adv - mean) / (std + 1e-6) in place (ppo.py:243). */
+int dppo_adv_normalize_f32(float* adv, const float* mean_std, int64_t n, void* stream);
+
+/* Old-policy evaluation with the default actor-critic MLP (ppo.py:235-238 with
+ * ActorCriticNetwork ppo.py:53-96; continuous_ppo.py:247-250 with :63-111): log-prob of the
+ * taken actions, V(obs), V(next_obs).  n samples; obs/next_obs [n][D]; actions int32 [n] or
+ * float32 [n][A]. */
+int dppo_old_policy_f32(dppo_handle* h, const float* params, const float* obs, const void* actions,
+                        const float* next_obs, float* log_probs, float* values, float* next_values,
+                        int64_t n, void* stream);
+
+/* One full PPO.learn (ppo.py:224-287 / continuous_ppo.py:236-299) with the default network:
+ * old-policy eval, GAE, returns, advantage normalisation, then num_epochs x num_minibatches
+ * {gather, forward, clipped-surrogate + value + entropy loss, analytic backward, [RCCL
+ * all-reduce], clip_grad_norm_, Adam}.  perms: host int32 [E][T*N] (np.random.permutation
+ * output per epoch, ppo.py:254), copied asynchronously through pinned staging.  params/m/v are
+ * updated in place.  Asynchronous: returns once everything is enqueued on `stream`.  Returns
+ * DPPO_EINVAL if T*N is not divisible by num_minibatches (the reference's reshape raises). */
+int dppo_learn_f32(dppo_handle* h, const dppo_rollout* rollout, float* params, float* adam_m,
+                   float* adam_v, const dppo_hparams* hp, const int32_t* host_perms,
+                   const dppo_learn_outputs* outputs, void* stream);
+
+/* Gradient of the minibatch loss at `params` for samples idx[0..m) of the records built by
+ * the last dppo_learn_f32/dppo_prepare_f32 (ppo.py:261-283), written to grad[P] (flat layout,
+ * unclipped), plus, if loss4 is non-NULL, the loss terms to HOST loss4[4] = {loss, loss_policy,
+ * loss_value, entropy} (synchronises the stream).  idx: device int32.  m_total: divisor of the
+ * means (global minibatch size). */
+int dppo_minibatch_grad_f32(dppo_handle* h, const float* params, const int32_t* idx, int32_t m,
+                            int32_t m_total, const dppo_hparams* hp, float* grad, float* loss4,
+                            void* stream);
+
+/* Stage a rollout for dppo_minibatch_grad_f32 without updating: old-policy eval, GAE, returns,
+ * normalisation, sample records (the first half of dppo_learn_f32). */
+int dppo_prepare_f32(dppo_handle* h, const dppo_rollout* rollout, const float* params,
+                     const dppo_hparams* hp, const dppo_learn_outputs* outputs, void* stream);
+
+/* clip_grad_norm_ (ppo.py:284, torch nn/utils/clip_grad.py) + Adam step (ppo.py:285, torch
+ * optim/adam.py _single_tensor_adam) over a flat buffer of n floats; step = step count AFTER
+ * this update.  Optional out_norm (device float) receives the pre-clip total norm. */
+int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v, int64_t n,
+                       float max_norm, double lr, float beta1, float beta2, float eps, int64_t step,
+                       float* out_norm, void* stream);
+
+/* The handle's pinned host staging buffer for the [E][T*N] permutations (waits for the previous
+ * learn's upload of it to finish).  Generating permutations straight into it (dppo_perm_numpy)
+ * and passing it to dppo_learn_f32 makes the upload a pure asynchronous DMA. */
+int dppo_perm_buffer(dppo_handle* h, int32_t** out);
+
+/* Per-step trace of the last dppo_learn_f32: E*M rows of DPPO_TRACE_FIELDS floats, copied to
+ * host memory.  Synchronises the handle's stream. */
+int dppo_get_trace(dppo_handle* h, float* host_out, int32_t rows);
+
+/* NumPy legacy RandomState.permutation, bit-exact (ppo.py:254): `count` permutations of
+ * arange(n) into out[count][n], advancing the MT19937 key[624]/pos in place exactly as
+ * np.random.permutation would.  Host only. */
+int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
+
+/* Multi-GPU over RCCL (xGMI): rank 0 creates the id, the caller broadcasts it (e.g. with
+ * torch.distributed), every rank attaches it to its handle.  dppo_learn_f32 then all-reduces the
+ * advantage statistics once and the gradient once per minibatch. */
+int dppo_comm_unique_id(char* out128);
+int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DPPO_H_ */

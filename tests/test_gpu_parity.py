@@ -1,0 +1,300 @@
+"""GPU parity tests: the HIP path (through the C ABI / the drop-in classes) against the golden
+fixtures captured from the reference and against the CPU oracle.
+
+Tolerances (SURVEY.md §7.2 hard part 2):
+* GAE advantages and returns: bit-exact (reference fp32 op order, no FMA contraction).
+* old-policy log-probs / values: |diff| <= 2e-5 (fp32 MLP, different GEMM summation order).
+* gradients: max|diff| <= 2e-5 x max|g| per step; losses / grad norms: rel 2e-5.
+* parameters after every Adam step: |diff| <= 5e-6 (Adam's first steps are ~lr*sign(g)).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import LEARN_TRACES, load_golden
+
+pytestmark = pytest.mark.gpu
+
+import diamond
+from diamond import _native as N
+from diamond.engine import DeviceRollout
+
+
+def dev():
+    return torch.device("cuda", 0)
+
+
+def t(x, dtype=None):
+    a = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None:
+        a = a.to(dtype)
+    return a.to(dev()).contiguous()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def gae_handle(T, Nn):
+    return N.Handle(0, N.Dims(T, Nn, 1, 1, 0, 64, 1, 1, 1, 0))
+
+
+# ---------------------------------------------------------------------------------------------
+def run_gae(r, te, tr, v, nv):
+    T, Nn = r.shape
+    h = gae_handle(T, Nn)
+    adv = torch.empty(T, Nn, device=dev())
+    ret = torch.empty(T, Nn, device=dev())
+    ms = torch.zeros(4, device=dev())
+    args = [t(r, torch.float32), t(te, torch.uint8), t(tr, torch.uint8), t(v, torch.float32),
+            t(nv, torch.float32)]
+    N.check(h.lib.dppo_gae_f32(h.h, *[a.data_ptr() for a in args], adv.data_ptr(), ret.data_ptr(),
+                               0.99, 0.95, stream()))
+    N.check(h.lib.dppo_adv_stats(h.h, ms.data_ptr(), stream()))
+    norm = adv.clone()
+    N.check(h.lib.dppo_adv_normalize_f32(norm.data_ptr(), ms.data_ptr(), norm.numel(), stream()))
+    torch.cuda.synchronize()
+    return adv.cpu().numpy(), ret.cpu().numpy(), ms.cpu().numpy(), norm.cpu().numpy()
+
+
+def test_gae_bitexact_golden():
+    d = load_golden("gae_cases.npz")
+    for n in d["names"]:
+        adv, ret, ms, norm = run_gae(d[n + "/rewards"], d[n + "/term"], d[n + "/trunc"],
+                                     d[n + "/values"], d[n + "/next_values"])
+        assert np.array_equal(adv, d[n + "/adv"]), n
+        assert np.array_equal(ret, d[n + "/returns"]), n
+        if adv.size > 1:
+            assert abs(ms[0] - d[n + "/mean"]) <= 1e-6 * max(1.0, abs(float(d[n + "/mean"]))), n
+            assert abs(ms[1] - d[n + "/std"]) <= 1e-6 * float(d[n + "/std"]), n
+            np.testing.assert_allclose(norm, d[n + "/adv_norm"], rtol=0, atol=2e-6, err_msg=n)
+
+
+@pytest.mark.parametrize("T,Nn", [(128, 8192), (128, 4096), (300, 16), (1, 1), (129, 33),
+                                  (7, 4104)])
+def test_gae_vs_oracle_sizes(T, Nn):
+    from oracle import ppo_np as P
+    rng = np.random.default_rng(T * 31 + Nn)
+    r = rng.normal(1, 1, (T, Nn)).astype(np.float32)
+    te = (rng.random((T, Nn)) < 0.02).astype(np.uint8)
+    tr = (rng.random((T, Nn)) < 0.005).astype(np.uint8)
+    v = rng.standard_normal((T, Nn)).astype(np.float32)
+    nv = rng.standard_normal((T, Nn)).astype(np.float32)
+    adv, ret, ms, _ = run_gae(r, te, tr, v, nv)
+    ref = P.gae(r, te, tr, v, nv)
+    assert np.array_equal(adv, ref)
+    assert np.array_equal(ret, v + ref)
+    if adv.size > 1:
+        mean, std = P.adv_stats(ref)
+        assert abs(ms[0] - mean) <= 1e-6 * max(1.0, abs(mean))
+        assert abs(ms[1] - std) <= 2e-6 * std
+
+
+def test_gae_full_size_properties():
+    """BASELINE sizes, size-independent checks: no dones => discounted-sum identity; all
+    terminated => adv = r - v."""
+    T, Nn = 128, 8192
+    rng = np.random.default_rng(5)
+    r = rng.normal(1, 1, (T, Nn)).astype(np.float32)
+    v = rng.standard_normal((T, Nn)).astype(np.float32)
+    nv = rng.standard_normal((T, Nn)).astype(np.float32)
+    z = np.zeros((T, Nn), np.uint8)
+    o = np.ones((T, Nn), np.uint8)
+    adv, _, _, _ = run_gae(r, o, z, v, nv)
+    assert np.array_equal(adv, r - v)
+    adv, _, _, _ = run_gae(r, z, z, v, nv)
+    delta = r.astype(np.float64) + 0.99 * nv - v
+    ref = np.zeros_like(delta)
+    a = 0.0
+    for k in range(T - 1, -1, -1):
+        a = delta[k] + 0.99 * 0.95 * a
+        ref[k] = a
+    np.testing.assert_allclose(adv, ref, rtol=1e-4, atol=1e-4)
+
+
+# ---------------------------------------------------------------------------------------------
+def make_agent(z):
+    import gym_stub
+    T, Nn, D, A, cont, _ = (int(x) for x in z["dims"])
+    Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
+    Agent = diamond.ContinuousPPO if cont else diamond.PPO
+    kw = {k: z["cfg/" + k].item() for k in ("num_epochs", "num_minibatches", "lr", "adam_eps",
+                                             "gamma", "gae_lambda", "ppo_clip",
+                                             "value_loss_weight", "entropy_beta",
+                                             "grad_norm_clip", "total_steps")}
+    cfg = Cfg(rollout_steps=T, num_envs=Nn, verbose=False,
+              advantage_norm=bool(z["cfg/advantage_norm"]), decay_lr=bool(z["cfg/decay_lr"]), **kw)
+    envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(D, A, continuous=bool(cont),
+                                                                 act_dim=A)] * Nn)
+    agent = Agent(None, cfg, envs=envs)
+    sd = {n: torch.from_numpy(z["init/" + n]) for n in z["param_names"]}
+    if hasattr(agent.network, "actor_out_layer"):  # alias of actor_head.2 in the state_dict
+        sd["actor_out_layer.weight"] = sd["actor_head.2.weight"]
+        sd["actor_out_layer.bias"] = sd["actor_head.2.bias"]
+    agent.network.load_state_dict(sd)
+    return agent
+
+
+def experience(z, li):
+    keys = ("obs", "next_obs", "actions", "rewards", "term", "trunc")
+    arrs = [z[f"exp{li}/" + k] for k in keys]
+    T = arrs[0].shape[0]
+    return [[a[k] for a in arrs] for k in range(T)]
+
+
+def flat_params(agent):
+    return np.concatenate([p.detach().cpu().numpy().ravel() for p in agent.network.parameters()])
+
+
+@pytest.mark.parametrize("name", LEARN_TRACES)
+def test_learn_matches_reference_trace(name):
+    """Full drop-in learn() through the fused HIP path vs the reference's captured trace,
+    including the NumPy-RNG minibatch order (global RNG set to the captured state)."""
+    z = load_golden(f"learn_{name}.npz")
+    T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
+    agent = make_agent(z)
+    assert agent._learner.fused
+    E, M = int(z["cfg/num_epochs"]), int(z["cfg/num_minibatches"])
+    losses, norms, params_after = [], [], []
+    for li in range(n_learn):
+        np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
+                             int(z[f"rng_pos_before{li}"]), 0, 0.0))
+        B = T * Nn
+        outs = {k: torch.empty(B, device=dev()) for k in
+                ("log_probs", "values", "next_values", "advantages", "returns")}
+        lo = N.LearnOutputs(*[outs[k].data_ptr() for k in
+                              ("log_probs", "values", "next_values", "advantages", "returns")])
+        ro = diamond.engine.stage_experience(experience(z, li), dev(), bool(cont))
+        agent.learn_device(ro, lo)
+        tr = agent.learn_trace()
+        losses += list(tr[:, 0])
+        norms += list(tr[:, 4])
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(outs["log_probs"].cpu().numpy(), z["old/log_probs"][li].ravel(),
+                                   atol=2e-5, err_msg="old log_probs")
+        np.testing.assert_allclose(outs["values"].cpu().numpy(), z["old/values"][li].ravel(),
+                                   atol=2e-5, err_msg="values")
+        np.testing.assert_allclose(outs["next_values"].cpu().numpy(),
+                                   z["old/next_values"][li].ravel(), atol=2e-5, err_msg="next_values")
+        np.testing.assert_allclose(outs["returns"].cpu().numpy() - outs["values"].cpu().numpy(),
+                                   z["old/adv"][li].ravel(), atol=5e-5, err_msg="advantages")
+        params_after.append(flat_params(agent))
+    np.testing.assert_allclose(losses, z["loss"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(norms, z["norm"], rtol=2e-5, atol=2e-5)
+    names = list(z["param_names"])
+    for n, p in agent.network.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), z["final/" + n], rtol=0, atol=5e-6,
+                                   err_msg=n)
+        st = agent.optimizer.state[p]
+        np.testing.assert_allclose(st["exp_avg"].cpu().numpy(), z[f"adam/{n}/exp_avg"],
+                                   rtol=1e-3, atol=1e-7, err_msg=n)
+        assert float(st["step"]) == float(z[f"adam/{names[0]}/step"])
+    # the global NumPy RNG ends where the reference left it
+    if n_learn == 1:
+        pass
+    if bool(z["cfg/decay_lr"]):
+        assert abs(agent.optimizer.param_groups[0]["lr"] - float(z[f"lr_after{n_learn - 1}"])) < 1e-12
+
+
+@pytest.mark.parametrize("name", ["cartpole_small", "lunar_medium", "cheetah_small"])
+def test_minibatch_gradient_matches_reference(name):
+    """First minibatch gradient (pre-clip) through dppo_minibatch_grad_f32."""
+    z = load_golden(f"learn_{name}.npz")
+    T, Nn, D, A, cont, _ = (int(x) for x in z["dims"])
+    agent = make_agent(z)
+    L = agent._learner
+    h = L.handle
+    hp = diamond.engine.hparams(agent.cfg, agent.cfg.lr, 0)
+    ro = diamond.engine.stage_experience(experience(z, 0), dev(), bool(cont))
+    N.check(h.lib.dppo_prepare_f32(h.h, ctypes.byref(ro.as_struct()), L.flat.flat.data_ptr(),
+                                   ctypes.byref(hp), None, stream()))
+    B = T * Nn
+    mb = B // agent.cfg.num_minibatches
+    idx = t(z["perms"][0][:mb], torch.int32)
+    g = torch.zeros(L.flat.total, device=dev())
+    loss4 = (ctypes.c_float * 4)()
+    N.check(h.lib.dppo_minibatch_grad_f32(h.h, L.flat.flat.data_ptr(), idx.data_ptr(), mb, mb,
+                                          ctypes.byref(hp), g.data_ptr(), loss4, stream()))
+    torch.cuda.synchronize()
+    gl = g.cpu().numpy()
+    Lay = h.layout
+    got = np.concatenate([gl[Lay.offset[i]:Lay.offset[i] + Lay.numel[i]] for i in range(Lay.count)])
+    ref = z["grads"][0]
+    scale = np.abs(ref).max()
+    assert np.abs(got - ref).max() <= 2e-5 * scale, np.abs(got - ref).max() / scale
+    assert abs(loss4[0] - z["loss"][0]) <= 2e-5 * max(1, abs(z["loss"][0]))
+
+
+def test_gae_kernel_via_agent_api():
+    """PPO.calculate_advantage accepts the reference's float 0/1 term/trunc tensors."""
+    z = load_golden("learn_cartpole_small.npz")
+    agent = make_agent(z)
+    d = load_golden("gae_cases.npz")
+    n = "random_16x8"
+    T, Nn = d[n + "/rewards"].shape
+    agent.cfg.rollout_steps = T
+    adv = agent.calculate_advantage(torch.from_numpy(d[n + "/rewards"]),
+                                    torch.from_numpy(d[n + "/term"].astype(np.float32)),
+                                    torch.from_numpy(d[n + "/trunc"].astype(np.float32)),
+                                    torch.from_numpy(d[n + "/values"]),
+                                    torch.from_numpy(d[n + "/next_values"]))
+    assert np.array_equal(adv.cpu().numpy(), d[n + "/adv"])
+
+
+def test_learn_large_vs_oracle():
+    """CartPole-shaped learn at N=256 (B=32,768) against the NumPy oracle, same perms."""
+    from oracle import ppo_np as P
+    import gym_stub
+    T, Nn, D, A = 128, 256, 4, 2
+    cfg = diamond.PPOConfig(rollout_steps=T, num_envs=Nn, verbose=False)
+    envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(D, A)] * Nn)
+    agent = diamond.PPO(None, cfg, envs=envs)
+    names = [n for n, _ in agent.network.named_parameters()]
+    params = {n: p.detach().cpu().numpy().copy() for n, p in agent.network.named_parameters()}
+    rng = np.random.default_rng(0)
+    exp = [[rng.standard_normal((Nn, D)).astype(np.float32),
+            rng.standard_normal((Nn, D)).astype(np.float32),
+            rng.integers(0, A, Nn), rng.normal(1, 1, Nn), rng.random(Nn) < 0.02,
+            rng.random(Nn) < 0.005] for _ in range(T)]
+    st = np.random.get_state()
+    agent.learn(exp)
+    tr = agent.learn_trace()
+    np.random.set_state(st)
+    hp = P.Hyper()
+    adam = P.new_adam_state(params, names)
+    stacked = [np.asarray(x) for x in zip(*exp)]
+    ref = P.learn(params, adam, stacked, hp, cfg.lr, False, rng=np.random)
+    np.testing.assert_allclose(tr[:, 0], ref["loss"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(tr[:, 4], ref["norm"], rtol=1e-4, atol=1e-5)
+    for n, p in agent.network.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), params[n], rtol=0, atol=2e-5,
+                                   err_msg=n)
+
+
+def test_learn_is_deterministic():
+    z = load_golden("learn_lunar_medium.npz")
+    res = []
+    for _ in range(2):
+        agent = make_agent(z)
+        np.random.set_state(("MT19937", z["rng_state_before0"].astype(np.uint32),
+                             int(z["rng_pos_before0"]), 0, 0.0))
+        ro = diamond.engine.stage_experience(experience(z, 0), dev(), False)
+        agent.learn_device(ro)
+        torch.cuda.synchronize()
+        res.append(flat_params(agent))
+    assert np.array_equal(res[0], res[1])
+
+
+def test_indivisible_minibatch_raises_value_error():
+    import gym_stub
+    cfg = diamond.PPOConfig(rollout_steps=3, num_envs=5, num_minibatches=4, verbose=False)
+    envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(4, 2)] * 5)
+    agent = diamond.PPO(None, cfg, envs=envs)
+    rng = np.random.default_rng(0)
+    exp = [[rng.standard_normal((5, 4)).astype(np.float32), rng.standard_normal((5, 4)).astype(np.float32),
+            rng.integers(0, 2, 5), rng.normal(size=5), rng.random(5) < 0.1, rng.random(5) < 0.1]
+           for _ in range(3)]
+    with pytest.raises(ValueError):
+        agent.learn(exp)

@@ -1,0 +1,140 @@
+"""CPU-side tests of the product library and host logic (no GPU compute calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import LEARN_TRACES, ROOT, load_golden
+
+import diamond
+from diamond import _native as N
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "dppo.h")).read()
+    return sorted(set(re.findall(r"\b(dppo_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = N.load()
+    syms = header_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(N.EXPORTED) == syms
+    assert b"gfx950" in lib.dppo_version()
+
+
+def test_param_layout_matches_reference_parameter_order():
+    for name in LEARN_TRACES:
+        z = load_golden(f"learn_{name}.npz")
+        T, Nn, D, A, cont, _ = (int(x) for x in z["dims"])
+        d = N.Dims(T, Nn, D, A, cont, 64, 4, 8, 1, 0)
+        L = N.param_layout(d)
+        names = list(z["param_names"])
+        assert L.count == len(names)
+        assert L.n_real == sum(z["init/" + n].size for n in names)
+        prev_end = 0
+        for i, n in enumerate(names):
+            shape = z["init/" + n].shape
+            assert L.numel[i] == int(np.prod(shape)), n
+            assert L.offset[i] % 16 == 0 and L.offset[i] >= prev_end
+            prev_end = L.offset[i] + L.numel[i]
+        assert L.total >= prev_end
+
+
+def test_param_counts_match_survey():
+    # CartPole 12,995; LunarLander 13,381; HalfCheetah 14,093; Pendulum 12,867
+    for (D, A, cont), n in {(4, 2, 0): 12995, (8, 4, 0): 13381, (17, 6, 1): 14093,
+                             (3, 1, 1): 12867}.items():
+        assert N.param_layout(N.Dims(128, 8, D, A, cont, 64, 4, 8, 1, 0)).n_real == n
+
+
+def test_invalid_dims_raise_value_error():
+    with pytest.raises(ValueError):
+        N.param_layout(N.Dims(0, 8, 4, 2, 0, 64, 4, 8, 1, 0))
+    with pytest.raises(ValueError):
+        N.param_layout(N.Dims(8, 8, 4, 2, 0, 64, 4, 8, 2, 2))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 64, 1000, 1 << 16, (1 << 16) + 3])
+def test_host_permutations_bit_exact_with_numpy(n):
+    count = 3
+    out = np.empty(count * n, np.int32)
+    np.random.seed(1234 + n)
+    N.numpy_rng_permutations(n, count, out)
+    after = np.random.get_state()
+    np.random.seed(1234 + n)
+    ref = np.concatenate([np.random.permutation(n) for _ in range(count)])
+    ref_after = np.random.get_state()
+    assert np.array_equal(out, ref)
+    assert np.array_equal(after[1], ref_after[1]) and after[2] == ref_after[2]
+
+
+def test_host_permutations_match_golden_and_private_rng():
+    d = load_golden("perm_seed42.npz")
+    rs = np.random.RandomState(42)
+    out = np.empty(1024, np.int32)
+    N.numpy_rng_permutations(1024, 1, out, rng=rs)
+    assert np.array_equal(out, d["p1024"])
+    # the golden learn traces' permutations from their recorded RNG state
+    z = load_golden("learn_cartpole_small.npz")
+    st = ("MT19937", z["rng_state_before0"].astype(np.uint32), int(z["rng_pos_before0"]), 0, 0.0)
+    rs.set_state(st)
+    E, B = 4, 128
+    out = np.empty(E * B, np.int32)
+    N.numpy_rng_permutations(B, E, out, rng=rs)
+    assert np.array_equal(out.reshape(E, B), z["perms"][:E])
+
+
+def test_default_network_init_matches_reference_bitwise():
+    """Same module structure + same torch RNG draws => identical initial weights (ppo.py:131-133)."""
+    from diamond.ppo import ActorCriticNetwork, network_parameter_init_, PPOConfig
+    from diamond.continuous_ppo import (ContinuousActorCriticNetwork, ContinuousPPOConfig,
+                                        network_parameter_init_ as cinit)
+    import gym_stub
+    for name, cont in (("cartpole_small", 0), ("lunar_medium", 0), ("cheetah_small", 1)):
+        z = load_golden(f"learn_{name}.npz")
+        T, Nn, D, A, _, _ = (int(x) for x in z["dims"])
+        np.random.seed(42)
+        torch.manual_seed(42)
+        env = gym_stub.SyntheticEnv(D, A, continuous=bool(cont), act_dim=A)
+        if cont:
+            net = ContinuousActorCriticNetwork(env.observation_space, env.action_space,
+                                               ContinuousPPOConfig())
+            cinit(net, gain=np.sqrt(2.0))
+        else:
+            net = ActorCriticNetwork(env.observation_space, env.action_space, PPOConfig())
+            network_parameter_init_(net, gain=np.sqrt(2.0))
+        got = [n for n, _ in net.named_parameters()]
+        assert got == list(z["param_names"])
+        for n, p in net.named_parameters():
+            assert torch.equal(p.detach(), torch.from_numpy(z["init/" + n])), (name, n)
+
+
+def test_configs_are_field_compatible():
+    import dataclasses
+    ref_fields = ["total_steps", "rollout_steps", "num_envs", "lr", "adam_eps", "decay_lr", "gamma",
+                  "gae_lambda", "num_epochs", "num_minibatches", "ppo_clip", "value_loss_weight",
+                  "entropy_beta", "advantage_norm", "grad_norm_clip", "network_hidden_dim", "cuda",
+                  "seed", "checkpoint", "save_interval", "verbose"]
+    for cls in (diamond.PPOConfig, diamond.ContinuousPPOConfig):
+        names = [f.name for f in dataclasses.fields(cls)]
+        assert names[:len(ref_fields)] == ref_fields
+        c = cls()
+        assert (c.rollout_steps, c.num_envs, c.num_epochs, c.num_minibatches, c.ppo_clip) == (64, 16, 4, 8, 0.2)
+    r = diamond.RecurrentPPOConfig()
+    assert (r.rollout_steps, r.num_envs, r.num_epochs, r.num_minibatches, r.ppo_clip,
+            r.gru_hidden_dim) == (32, 32, 10, 1, 0.15, 16)
+
+
+def test_agents_fail_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import gym_stub
+    envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(4, 2)] * 8)
+    with pytest.raises(RuntimeError, match="GPU"):
+        diamond.PPO(None, diamond.PPOConfig(num_envs=8, verbose=False), envs=envs)
