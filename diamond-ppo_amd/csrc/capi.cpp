@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "common.h"
 
@@ -70,13 +71,22 @@ struct dppo_handle {
   float *logp = nullptr, *values = nullptr, *next_values = nullptr, *adv = nullptr,
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
-  double *partials = nullptr, *dsum = nullptr;
+  double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
   int32_t* perms_dev = nullptr;
   int32_t* perms_pinned = nullptr;
   hipEvent_t perm_copy_done = nullptr;
   bool perm_copy_pending = false;
   int32_t trace_rows = 0;
   hipStream_t last_stream = nullptr;
+  // optional per-kernel-class timing with HIP events on the launch stream
+  bool timing = false;
+  struct Rec {
+    int cls;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
   // RCCL
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -167,6 +177,40 @@ int dalloc(T** p, int64_t n) {
 
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
+enum KClass { K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_NCLASS };
+
+hipEvent_t pool_event(dppo_handle* h) {
+  if (h->pool_used == h->pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    h->pool.push_back(e);
+  }
+  return h->pool[h->pool_used++];
+}
+
+// RAII bracket: records a start/stop event pair around one launch when timing is enabled.
+struct Timed {
+  dppo_handle* h;
+  hipStream_t s;
+  int cls;
+  hipEvent_t a = nullptr;
+  Timed(dppo_handle* h_, int cls_, hipStream_t s_) : h(h_), s(s_), cls(cls_) {
+    if (h->timing) {
+      a = pool_event(h);
+      if (a) (void)hipEventRecord(a, s);
+    }
+  }
+  ~Timed() {
+    if (h->timing && a) {
+      hipEvent_t b = pool_event(h);
+      if (b) {
+        (void)hipEventRecord(b, s);
+        h->recs.push_back({cls, a, b});
+      }
+    }
+  }
+};
+
 int require_mlp(const dppo_handle* h) {
   if (!h->mlp_ok) {
     set_error("fused MLP kernels support hidden=64, obs_dim<=32, act_dim<=16 (got H=%d D=%d A=%d)",
@@ -192,16 +236,28 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
   }
   const dppo_dims& d = h->dims;
   // (2) old-policy evaluation (ppo.py:235-238)
-  DPPO_TRY(launch_eval(h->sh, h->po, params, ro->obs, ro->actions, ro->next_obs, h->logp,
-                       h->values, h->next_values, h->B, s));
+  {
+    Timed tm(h, K_EVAL, s);
+    DPPO_TRY(launch_eval(h->sh, h->po, params, ro->obs, ro->actions, ro->next_obs, h->logp,
+                         h->values, h->next_values, h->B, s));
+  }
   // (3) GAE + returns (ppo.py:240-241)
-  DPPO_TRY(launch_gae(ro->rewards, ro->term, ro->trunc, h->values, h->next_values, h->adv, h->ret,
-                      h->partials, d.rollout_steps, d.num_envs, hp->gamma, hp->gae_lambda, s,
-                      &h->n_partials));
+  {
+    Timed tm(h, K_GAE, s);
+    DPPO_TRY(launch_gae(ro->rewards, ro->term, ro->trunc, h->values, h->next_values, h->adv,
+                        h->ret, h->partials, d.rollout_steps, d.num_envs, hp->gamma,
+                        hp->gae_lambda, s, &h->n_partials));
+  }
   // (4) advantage statistics, global over ranks (ppo.py:243)
   if (hp->advantage_norm) {
-    DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, s));
-    DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, s));
+    {
+      Timed tm(h, K_STATS, s);
+      DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, s));
+    }
+    if (h->comm && h->nranks > 1) {
+      Timed tm(h, K_COMM, s);
+      DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, s));
+    }
   }
   // (5) sample records for the minibatch gather (ppo.py:246-249)
   PackArgs pa{};
@@ -221,7 +277,10 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
   pa.A = d.act_dim;
   pa.R = h->sh.R;
   pa.continuous = d.continuous;
-  DPPO_TRY(launch_pack(pa, s));
+  {
+    Timed tm(h, K_PACK, s);
+    DPPO_TRY(launch_pack(pa, s));
+  }
   if (out) {
     const size_t nb = (size_t)h->B * sizeof(float);
     if (out->log_probs)
@@ -255,13 +314,22 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int3
   ga.slabs = h->slabs;
   ga.slab_stride = h->slab_stride;
   ga.p_total = h->layout.total;
-  int G = grad_grid(m);
+  int G = mb_grid(m);
   if (G > h->G) G = h->G;
-  DPPO_TRY(launch_grad(h->sh, h->po, ga, G, s));
-  DPPO_TRY(launch_slab_reduce(h->slabs, G, h->slab_stride, h->layout.total, h->grad, nullptr,
-                              ga.inv_m, h->po.ls, d.continuous ? d.act_dim : 0, hp->entropy_beta,
-                              (d.continuous && h->rank == 0) ? 1 : 0, s));
-  DPPO_TRY(allreduce(h, h->grad, (size_t)h->layout.total + 8, ncclFloat32, s));
+  {
+    Timed tm(h, K_GRAD, s);
+    DPPO_TRY(launch_mb(h->sh, h->po, ga, G, s));
+  }
+  {
+    Timed tm(h, K_REDUCE, s);
+    DPPO_TRY(launch_slab_reduce(h->slabs, G, h->slab_stride, h->layout.total, h->grad, h->sq_part,
+                                h->po.ls, d.continuous ? d.act_dim : 0, hp->entropy_beta,
+                                (d.continuous && h->rank == 0) ? 1 : 0, s));
+  }
+  if (h->comm && h->nranks > 1) {
+    Timed tm(h, K_COMM, s);
+    DPPO_TRY(allreduce(h, h->grad, (size_t)h->layout.total + 8, ncclFloat32, s));
+  }
   return DPPO_OK;
 }
 
@@ -306,9 +374,9 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   h->sh.continuous = dims->continuous;
   h->sh.R = D8 + 4 + (dims->continuous ? (dims->act_dim + 3) / 4 * 4 : 0);
   h->mlp_ok = dims->hidden == 64 && dims->obs_dim <= 32 && dims->act_dim <= 16 &&
-              mlp_lds_bytes_grad(h->sh) <= 160 * 1024 &&
+              mb_lds_bytes(h->sh) <= 160 * 1024 &&
               (size_t)(h->layout.total + 8) * 4 <= 160 * 1024;
-  h->G = grad_grid(h->mb > 0 ? h->mb : 1);
+  h->G = mb_grid(h->mb > 0 ? h->mb : 1);
   h->slab_stride = round_up(h->layout.total + 8, 64);
   const int64_t E = dims->num_epochs, M = dims->num_minibatches;
   h->trace_rows = (int32_t)(E * M);
@@ -329,6 +397,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->mean_std, 4));
   chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
   chk(dalloc(&h->dsum, 4));
+  chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
   chk(dalloc(&h->perms_dev, E * h->B));
   if (rc == DPPO_OK) {
     hipError_t e = hipHostMalloc((void**)&h->perms_pinned, (size_t)(E * h->B) * sizeof(int32_t),
@@ -373,9 +442,11 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->mean_std);
   (void)hipFree(h->partials);
   (void)hipFree(h->dsum);
+  (void)hipFree(h->sq_part);
   (void)hipFree(h->perms_dev);
   if (h->perms_pinned) (void)hipHostFree(h->perms_pinned);
   if (h->perm_copy_done) (void)hipEventDestroy(h->perm_copy_done);
+  for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
   delete h;
 }
 
@@ -476,9 +547,8 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
   const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
   const double step_size = lr / bc1;
   const double bc2_sqrt = std::pow(bc2, 0.5);
-  return launch_clip_adam(params, grad, adam_m, adam_v, n, max_norm, (float)lr,
-                          (float)(-step_size), (float)bc2_sqrt, beta1, beta2, eps, out_norm,
-                          S(stream));
+  return launch_clip_adam(params, grad, adam_m, adam_v, n, max_norm, (float)(-step_size),
+                          (float)bc2_sqrt, beta1, beta2, eps, out_norm, S(stream));
 }
 
 int dppo_learn_f32(dppo_handle* h, const dppo_rollout* rollout, float* params, float* adam_m,
@@ -523,8 +593,14 @@ int dppo_learn_f32(dppo_handle* h, const dppo_rollout* rollout, float* params, f
       const double bc2 = 1.0 - std::pow((double)hp->adam_beta2, step);
       const double step_size = hp->lr / bc1;
       const double bc2_sqrt = std::pow(bc2, 0.5);
+      Timed tm(h, K_ADAM, s);
+      // single device: the norm comes from the reduce kernel's per-block partials; after an
+      // all-reduce those are stale, so the Adam kernel recomputes it from the gradient
+      const bool multi = h->comm && h->nranks > 1;
       DPPO_TRY(launch_clip_adam_traced(params, h->grad, adam_m, adam_v, h->layout.total,
-                                       hp->grad_norm_clip, (float)hp->lr, (float)(-step_size),
+                                       multi ? nullptr : h->sq_part,
+                                       slab_reduce_blocks(h->layout.total), hp->grad_norm_clip,
+                                       (float)(-step_size),
                                        (float)bc2_sqrt, hp->adam_beta1, hp->adam_beta2,
                                        hp->adam_eps, nullptr, h->trace + k * DPPO_TRACE_FIELDS,
                                        inv_m, hp->value_loss_weight, hp->entropy_beta, s));
@@ -545,6 +621,39 @@ int dppo_perm_buffer(dppo_handle* h, int32_t** out) {
     h->perm_copy_pending = false;
   }
   *out = h->perms_pinned;
+  return DPPO_OK;
+}
+
+int dppo_set_timing(dppo_handle* h, int32_t enable) {
+  if (!h) {
+    set_error("null handle");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  DPPO_HIP_CHECK(hipDeviceSynchronize());
+  h->timing = enable != 0;
+  h->recs.clear();
+  h->pool_used = 0;
+  return DPPO_OK;
+}
+
+int dppo_get_timing(dppo_handle* h, double* ms_sum, int64_t* counts) {
+  if (!h || !ms_sum || !counts) {
+    set_error("null argument to dppo_get_timing");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  for (int k = 0; k < DPPO_TIMING_CLASSES; ++k) {
+    ms_sum[k] = 0.0;
+    counts[k] = 0;
+  }
+  for (const auto& r : h->recs) {
+    DPPO_HIP_CHECK(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    DPPO_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+    ms_sum[r.cls] += ms;
+    counts[r.cls] += 1;
+  }
   return DPPO_OK;
 }
 

@@ -79,19 +79,25 @@ struct GradArgs {
   int64_t p_total;
 };
 int grad_grid(int32_t m);
+// Feature-split fused minibatch kernel (mbstep.hip), the one learn() uses.
+size_t mb_lds_bytes(const MlpShape& sh);
+int mb_grid(int32_t m);
+int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
+              hipStream_t s);
 int launch_grad(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
                 hipStream_t s);
 
 // Optimiser kernels: optim.hip.
+int slab_reduce_blocks(int64_t p_total);
 int launch_slab_reduce(const float* slabs, int G, int64_t slab_stride, int64_t p_total,
-                       float* grad, float* loss4, float inv_m, int64_t ls_off, int ls_n,
-                       float ent_coef, int add_entropy_const, hipStream_t s);
+                       float* grad, double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
+                       int add_entropy_const, hipStream_t s);
 int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int64_t n,
-                            float max_norm, float lr, float neg_step_size, float bc2_sqrt,
-                            float beta1, float beta2, float eps, float* out_norm, float* trace,
-                            float inv_m, float vf, float ent, hipStream_t s);
+                            const double* sq_part, int n_sq, float max_norm, float neg_step_size,
+                            float bc2_sqrt, float beta1, float beta2, float eps, float* out_norm,
+                            float* trace, float inv_m, float vf, float ent, hipStream_t s);
 int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, float max_norm,
-                     float lr, float neg_step_size, float bc2_sqrt, float beta1, float beta2,
-                     float eps, float* out_norm, hipStream_t s);
+                     float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
+                     float* out_norm, hipStream_t s);
 
 }  // namespace dppo

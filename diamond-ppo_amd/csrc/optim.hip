@@ -6,27 +6,57 @@
 // reference runs: step += 1; exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
 // denom = sqrt(exp_avg_sq)/sqrt(bc2) + eps; p.addcdiv_(exp_avg, denom, -lr/bc1)).
 //
-// Both kernels are HBM/L2-latency bound and tiny (P ~ 13-14 K floats): the slab reduction reads
-// G slabs of P floats once (fixed order => bit-reproducible); every Adam workgroup recomputes the
-// global norm from the reduced gradient (52 KB, L2-resident) so no grid-wide sync is needed.
+// Both kernels are latency-bound, not bandwidth-bound (the slabs are G x P floats, ~13 MB at
+// G = 256; P ~ 13-14 K), so every thread keeps many independent loads in flight:
+//  * slab_reduce: one workgroup per 64 parameters; each of its 4 waves sums a quarter of the
+//    slabs for the 64 parameters (lane = parameter, 256 contiguous bytes per wave load, 16 loads
+//    in flight per lane), the four quarters are combined through LDS in a fixed order
+//    (bit-reproducible), and each block also emits its partial sum of squares.
+//  * clip_adam: the global norm comes from those per-block partials (fixed order) or, after an
+//    RCCL all-reduce changed the gradient, from the gradient itself with 8 loads in flight.
 #include "common.h"
 
 namespace dppo {
 namespace {
 
+constexpr int kRedParams = 64;  // parameters per slab_reduce workgroup
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, int G,
                                                           int64_t stride, int64_t p_total,
                                                           float* __restrict__ grad,
+                                                          double* __restrict__ sq_part,
                                                           int64_t ls_off, int ls_n, float ent_coef,
                                                           int add_entropy_const) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= p_total + 8) return;
+  __shared__ float part[4][kRedParams];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
+  const int64_t n = p_total + 8;
   float s = 0.0f;
-  for (int g = 0; g < G; ++g) s += slabs[(int64_t)g * stride + p];
-  // d(-beta * mean H)/d log_std = -beta per action dim (continuous_ppo.py:286-291): a constant
-  // the per-sample kernel does not see; added once (rank 0 only under data parallelism).
-  if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) s -= ent_coef;
-  grad[p] = s;
+  if (p < n) {
+    const float* src = slabs + p;
+    int g = wave;
+    // 16 independent loads per batch (slabs wave, wave+4, ...), summed in slab order
+    for (; g + 60 < G; g += 64) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = src[(int64_t)(g + 4 * k) * stride];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += v[k];
+    }
+    for (; g < G; g += 4) s += src[(int64_t)g * stride];
+  }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0) {
+    float t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    // d(-beta * mean H)/d log_std = -beta per action dim (continuous_ppo.py:286-291): a
+    // constant the per-sample kernel does not see; added once (rank 0 under data parallelism).
+    if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
+    if (p < n) grad[p] = t;
+    double q = (p < p_total) ? (double)t * (double)t : 0.0;
+    for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+    if (lane == 0) sq_part[blockIdx.x] = q;
+  }
 }
 
 __device__ __forceinline__ double block_sum(double v, double* sh) {
@@ -40,17 +70,27 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
 }
 
 // grad: [n] flat gradient followed by 8 loss slots {sum l_pi, sum l_v, sum H, ...}.
+// sq_part/n_sq: per-block partial sums of squares of grad (null => recompute from grad).
 __global__ __launch_bounds__(256) void clip_adam_kernel(
     float* __restrict__ params, float* __restrict__ grad, float* __restrict__ m,
-    float* __restrict__ v, int64_t n, float max_norm, float lr, float neg_step_size,
-    float bc2_sqrt, float beta1, float beta2, float eps, float* __restrict__ out_norm,
-    float* __restrict__ trace, float inv_m, float vf, float ent) {
+    float* __restrict__ v, int64_t n, const double* __restrict__ sq_part, int n_sq,
+    float max_norm, float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
+    float* __restrict__ out_norm, float* __restrict__ trace, float inv_m, float vf, float ent) {
 #pragma clang fp contract(off)
   __shared__ double sh[4];
   double sq = 0.0;
-  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
-    const double g = grad[k];
-    sq += g * g;
+  if (sq_part) {
+    for (int k = threadIdx.x; k < n_sq; k += blockDim.x) sq += sq_part[k];
+  } else {
+    int64_t k = threadIdx.x;
+    for (; k + 7 * 256 < n; k += 8 * 256) {
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = grad[k + j * 256];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq += (double)g[j] * (double)g[j];
+    }
+    for (; k < n; k += 256) sq += (double)grad[k] * (double)grad[k];
   }
   const double tot = block_sum(sq, sh);
   const float norm = (float)sqrt(tot);
@@ -88,36 +128,37 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
 
 }  // namespace
 
+int slab_reduce_blocks(int64_t p_total) { return (int)((p_total + 8 + kRedParams - 1) / kRedParams); }
+
 int launch_slab_reduce(const float* slabs, int G, int64_t slab_stride, int64_t p_total,
-                       float* grad, float* /*loss4*/, float /*inv_m*/, int64_t ls_off, int ls_n,
-                       float ent_coef, int add_entropy_const, hipStream_t s) {
-  const int64_t n = p_total + 8;
-  const unsigned grid = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, s, slabs, G, slab_stride,
-                     p_total, grad, ls_off, ls_n, ent_coef, add_entropy_const);
+                       float* grad, double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
+                       int add_entropy_const, hipStream_t s) {
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(slab_reduce_blocks(p_total)), dim3(256), 0, s,
+                     slabs, G, slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef,
+                     add_entropy_const);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
 
 int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int64_t n,
-                            float max_norm, float lr, float neg_step_size, float bc2_sqrt,
-                            float beta1, float beta2, float eps, float* out_norm, float* trace,
-                            float inv_m, float vf, float ent, hipStream_t s) {
+                            const double* sq_part, int n_sq, float max_norm, float neg_step_size,
+                            float bc2_sqrt, float beta1, float beta2, float eps, float* out_norm,
+                            float* trace, float inv_m, float vf, float ent, hipStream_t s) {
   int64_t g = (n + 255) / 256;
   if (g > 256) g = 256;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)g), dim3(256), 0, s, params, grad, m, v, n,
-                     max_norm, lr, neg_step_size, bc2_sqrt, beta1, beta2, eps, out_norm, trace,
-                     inv_m, vf, ent);
+                     sq_part, n_sq, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
+                     out_norm, trace, inv_m, vf, ent);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
 
 int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, float max_norm,
-                     float lr, float neg_step_size, float bc2_sqrt, float beta1, float beta2,
-                     float eps, float* out_norm, hipStream_t s) {
-  return launch_clip_adam_traced(params, grad, m, v, n, max_norm, lr, neg_step_size, bc2_sqrt,
-                                 beta1, beta2, eps, out_norm, nullptr, 0.f, 0.f, 0.f, s);
+                     float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
+                     float* out_norm, hipStream_t s) {
+  return launch_clip_adam_traced(params, grad, m, v, n, nullptr, 0, max_norm, neg_step_size,
+                                 bc2_sqrt, beta1, beta2, eps, out_norm, nullptr, 0.f, 0.f, 0.f, s);
 }
 
 }  // namespace dppo

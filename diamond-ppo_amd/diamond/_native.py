@@ -27,8 +27,9 @@ EXPORTED = [
     "dppo_gae_f32", "dppo_adv_stats", "dppo_adv_normalize_f32", "dppo_old_policy_f32",
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
-    "dppo_comm_init",
+    "dppo_comm_init", "dppo_set_timing", "dppo_get_timing",
 ]
+TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam", "allreduce"]
 
 
 class Dims(ctypes.Structure):
@@ -102,6 +103,8 @@ def load():
         "dppo_perm_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
+        "dppo_set_timing": (ctypes.c_int, [vp, i32]),
+        "dppo_get_timing": (ctypes.c_int, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -206,6 +209,16 @@ class Handle:
         out = np.zeros((rows, TRACE_FIELDS), np.float32)
         check(self.lib.dppo_get_trace(self.h, out.ctypes.data, int(rows)), "dppo_get_trace")
         return out
+
+    def set_timing(self, enable: bool):
+        check(self.lib.dppo_set_timing(self.h, int(bool(enable))), "dppo_set_timing")
+
+    def timing(self) -> dict:
+        """{class: (total_ms, launches)} since set_timing(True) (synchronises)."""
+        ms = np.zeros(len(TIMING_CLASSES), np.float64)
+        cnt = np.zeros(len(TIMING_CLASSES), np.int64)
+        check(self.lib.dppo_get_timing(self.h, ms.ctypes.data, cnt.ctypes.data), "dppo_get_timing")
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(TIMING_CLASSES)}
 
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         buf = ctypes.create_string_buffer(uid, 128)

@@ -167,6 +167,15 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
  * and passing it to dppo_learn_f32 makes the upload a pure asynchronous DMA. */
 int dppo_perm_buffer(dppo_handle* h, int32_t** out);
 
+/* Per-kernel timing with HIP events recorded on the launch stream around every launch the
+ * handle issues (off by default).  Classes, in order: old-policy eval, GAE, advantage-stat
+ * reduce, record pack, fused minibatch gradient, slab reduce, clip+Adam, RCCL all-reduce.
+ * dppo_set_timing() synchronises the device and clears the records; dppo_get_timing()
+ * synchronises and returns per-class summed milliseconds and launch counts. */
+#define DPPO_TIMING_CLASSES 8
+int dppo_set_timing(dppo_handle* h, int32_t enable);
+int dppo_get_timing(dppo_handle* h, double* ms_sum, int64_t* counts);
+
 /* Per-step trace of the last dppo_learn_f32: E*M rows of DPPO_TRACE_FIELDS floats, copied to
  * host memory.  Synchronises the handle's stream. */
 int dppo_get_trace(dppo_handle* h, float* host_out, int32_t rows);
