@@ -213,6 +213,10 @@ def main():
     torch.cuda.synchronize(device)
     h = agent._learner.handle
     h.set_timing(True)
+    hs = agent._learner.host_seconds
+    for k in ("perm_wait", "perms", "enqueue"):
+        hs[k] = 0.0
+    hs["calls"] = 0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -293,7 +297,12 @@ def main():
             "roofline": roofline,
             "kernels": kernel_ms,
             "device_ms_per_step": round(dev_ms / args.steps, 4),
+            "host_ms_per_step": {k: round(hs[k] / max(hs["calls"], 1) * 1e3, 4)
+                                 for k in ("perm_wait", "perms", "enqueue")},
             "final_loss": float(loss_trace[-1, 0]),
+            "device": {"name": torch.cuda.get_device_name(device),
+                       "arch": getattr(torch.cuda.get_device_properties(device), "gcnArchName", ""),
+                       "compute_units": torch.cuda.get_device_properties(device).multi_processor_count},
         }
     if rank == 0 and world == 1 and not args.no_gae_roofline:
         out["roofline_gae"] = gae_roofline(device)

@@ -65,6 +65,7 @@ struct dppo_handle {
   int64_t B = 0;   // local samples T*N
   int32_t mb = 0;  // local minibatch size B / M
   int G = 1;       // workgroups (= gradient slabs) of the fused minibatch kernel
+  int num_cus = 256;
   int64_t slab_stride = 0;
   int n_partials = 0;
   // device workspace
@@ -376,7 +377,15 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   h->mlp_ok = dims->hidden == 64 && dims->obs_dim <= 32 && dims->act_dim <= 16 &&
               mb_lds_bytes(h->sh) <= 160 * 1024 &&
               (size_t)(h->layout.total + 8) * 4 <= 160 * 1024;
+  // One fused-minibatch workgroup per CU (its LDS footprint admits exactly one): never launch
+  // more workgroups than CUs, or the surplus runs as a second, serialised round.
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  h->num_cus = cus;
   h->G = mb_grid(h->mb > 0 ? h->mb : 1);
+  if (h->G > cus) h->G = cus;
   h->slab_stride = round_up(h->layout.total + 8, 64);
   const int64_t E = dims->num_epochs, M = dims->num_minibatches;
   h->trace_rows = (int32_t)(E * M);
@@ -415,6 +424,8 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   if (rc == DPPO_OK) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
+    // the fused kernel never writes the layout's padding floats: keep them zero in every slab
+    (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }
   if (rc != DPPO_OK) {
     dppo_destroy(h);

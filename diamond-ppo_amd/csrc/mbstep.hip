@@ -40,6 +40,13 @@ constexpr int SD = 68;                                  // stride of the per-sam
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;
 
+// Timing-only ablation switches (tools/ablate.py); a shipped build defines none of them.
+#ifdef DPPO_ABL_NOBARRIER
+#define STEP_BARRIER() __builtin_amdgcn_wave_barrier()
+#else
+#define STEP_BARRIER() __syncthreads()
+#endif
+
 __host__ __device__ constexpr int perm(int k) { return (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3); }
 
 struct TeamLds {  // offsets (floats) of one team's images
@@ -116,34 +123,35 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 }
 
 __device__ __forceinline__ float tanh_f(float x) {
-  // tanh via one exp: t = e^{-2|x|}; tanh = sign(x) (1 - t) / (1 + t).  Relative error ~1e-7 for
-  // |x| > 0.1; below that 1-t cancels, so use the odd Taylor polynomial (error < 3e-8).
-  const float ax = fabsf(x);
-  float r;
-  if (ax < 0.0625f) {
-    const float x2 = x * x;
-    r = x * (1.0f + x2 * (-0.33333334f + x2 * (0.13333334f + x2 * -0.053968254f)));
-  } else {
-    const float t = __expf(-2.0f * ax);
-    r = copysignf((1.0f - t) / (1.0f + t), x);
-  }
-  return r;
+  // tanh via one exp and one hardware reciprocal, branch-free: t = e^{-2|x|},
+  // tanh = sign(x) (1 - t) / (1 + t).  Absolute error <= ~1.5e-7 over the whole range (1 - t
+  // cancels near 0, which costs relative but not absolute accuracy; activations are O(1)).
+#ifdef DPPO_ABL_NOTANH
+  return x * 0.5f;
+#endif
+  const float t = __expf(-2.0f * fabsf(x));
+  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
 }
 
 // One 16-row output slice for 2 sample tiles: acc[sb] += W(regs, k = 4t + h4) x X(LDS image).
 template <int NT>
 __device__ __forceinline__ void mm_rows(f32x4 (&acc)[NSB], const float (&w)[NT], const float* X,
                                         int stride, int l15, int h4) {
+#ifdef DPPO_ABL_NOMM
+  return;
+#endif
 #pragma unroll
   for (int q = 0; q < NT / 4; ++q) {
+    f32x4 b[NSB];
 #pragma unroll
-    for (int sb = 0; sb < NSB; ++sb) {
-      const f32x4 b = *(const f32x4*)(X + (16 * sb + l15) * stride + 16 * q + 4 * h4);
-      acc[sb] = mfma16(w[4 * q + 0], b[0], acc[sb]);
-      acc[sb] = mfma16(w[4 * q + 1], b[1], acc[sb]);
-      acc[sb] = mfma16(w[4 * q + 2], b[2], acc[sb]);
-      acc[sb] = mfma16(w[4 * q + 3], b[3], acc[sb]);
-    }
+    for (int sb = 0; sb < NSB; ++sb)
+      b[sb] = *(const f32x4*)(X + (16 * sb + l15) * stride + 16 * q + 4 * h4);
+    // consecutive MFMAs hit different accumulators (16x16x4 f32: 32-cycle issue, 40-cycle
+    // dependent latency)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int sb = 0; sb < NSB; ++sb) acc[sb] = mfma16(w[4 * q + j], b[sb][j], acc[sb]);
   }
 }
 
@@ -181,6 +189,9 @@ template <int NIB>
 __device__ __forceinline__ void wgrad16(f32x4* acc, const float* DZ, int dz_stride,
                                         int dz_col0, const float* X, int x_stride, int x_col0,
                                         int row0, int l15, int h4) {
+#ifdef DPPO_ABL_NOWGRAD
+  return;
+#endif
   const int ca = dz_col0 + perm(row0 + l15);
 #pragma unroll
   for (int t = 0; t < S / 4; ++t) {
@@ -314,7 +325,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       }
     }
     load_idx(step + gridDim.x);
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (2) layer 1
     f32x4 h1r[NSB], h2r[NSB], har[NSB], hcr[NSB];
@@ -327,14 +338,14 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     }
     tanh_rows(h1r);
     put_rows(H1, SA, row0, h1r, l15, h4);
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (3) layer 2
     init_bias(h2r, lds + L.b2, row0, h4);
     mm_rows<16>(h2r, w2f, H1, SA, l15, h4);
     tanh_rows(h2r);
     put_rows(H2, SA, row0, h2r, l15, h4);
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (4) actor / critic hidden layers
     init_bias(har, lds + L.ba, row0, h4);
@@ -345,9 +356,12 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     tanh_rows(hcr);
     put_rows(HAC, SAC, row0, har, l15, h4);
     put_rows(HAC, SAC, 64 + row0, hcr, l15, h4);
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (5) heads + loss (VALU, 8 lanes per sample)
+#ifdef DPPO_ABL_NOHEADS
+    if (step < 0)
+#endif
 #pragma unroll
     for (int pss = 0; pss < 2; ++pss) {
       const int hs = 16 * q + 8 * pss + (lane >> 3);
@@ -452,7 +466,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       if (hj == 0) drow[32] = dv;
     }
     load_rec(step + gridDim.x);
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (6) head weight gradients (lane = feature column) and dZa, dZc of this wave's rows
     {
@@ -491,7 +505,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       put_rows(DZAC, SAC, row0, dza, l15, h4);
       put_rows(DZAC, SAC, 64 + row0, dzc, l15, h4);
     }
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (7) dh2 = Wa^T dZa + Wc^T dZc ; dZ2 ; dWa, dWc of this wave's rows
     {
@@ -509,7 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       wgrad16<4>(gWa, DZAC, SAC, 0, H2, SA, 0, row0, l15, h4);
       wgrad16<4>(gWc, DZAC, SAC, 64, H2, SA, 0, row0, l15, h4);
     }
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (8) dh1 = W2^T dZ2 ; dZ1 ; dW2 of this wave's rows
     {
@@ -525,19 +539,20 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       put_rows(DZ1, SA, row0, dz1, l15, h4);
       wgrad16<4>(gW2, DZ2, SA, 0, H1, SA, 0, row0, l15, h4);
     }
-    __syncthreads();
+    STEP_BARRIER();
 
     // ---- (9) dW1 of this wave's rows (input = observations)
     if (nk1 == 8) wgrad16<2>(gW1, DZ1, SA, 0, X0, SX0, 0, row0, l15, h4);
     else wgrad16<1>(gW1, DZ1, SA, 0, X0, SX0, 0, row0, l15, h4);
-    __syncthreads();
+    STEP_BARRIER();
   }
 
-  // ---------------- epilogue: fixed-order reduction of all partials through LDS -> one slab
-  float* acc = lds_;
-  const int np = (int)a.p_total + 8;
-  for (int k = tid; k < np; k += kThreads) acc[k] = 0.0f;
-  // bias partials: sum over the 16 sample lanes of each row group
+  // ---------------- epilogue -> one slab per workgroup.  Each wave owns distinct rows of dW1,
+  // dW2, dWa, dWc and of the hidden biases, so it stores them straight to the slab (no cross-wave
+  // sum).  Only the head partials (lane = feature column, summed over this wave's samples) and
+  // the loss sums are combined across the 4 waves, through LDS in a fixed order.  Padding floats
+  // of the flat layout are never written (the slabs were zeroed at dppo_create).
+  float* slab = a.slabs + (int64_t)blockIdx.x * a.slab_stride;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -554,54 +569,56 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     s_v += __shfl_xor(s_v, off);
     s_ent += __shfl_xor(s_ent, off);
   }
-  __syncthreads();
-  const int fcol = lane;  // head-gradient lanes hold permuted feature column `lane`
-  int ftrue = 0;
-  {  // inverse of perm within the 16-block: col = 16b + 4(k&3) + ((k>>2)&3)
-    const int c = fcol & 15;
-    ftrue = (fcol & ~15) + 4 * (c & 3) + (c >> 2);
-  }
-  for (int w = 0; w < kTeams * kTeamWaves; ++w) {
-    if (wave == w) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = row0 + 4 * h4 + r;
+  for (int r = 0; r < 4; ++r) {
+    const int o = row0 + 4 * h4 + r;
 #pragma unroll
-        for (int ib = 0; ib < 4; ++ib) {
-          const int i = 16 * ib + l15;
-          acc[po.W2 + o * H + i] += gW2[ib][r];
-          acc[po.Wa + o * H + i] += gWa[ib][r];
-          acc[po.Wc + o * H + i] += gWc[ib][r];
-        }
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
-          const int i = 16 * ib + l15;
-          if (i < a.D) acc[po.W1 + o * a.D + i] += gW1[ib][r];
-        }
-        if (l15 == 0) {
-          acc[po.b1 + o] += gb[0][r];
-          acc[po.b2 + o] += gb[1][r];
-          acc[po.ba + o] += gb[2][r];
-          acc[po.bc + o] += gb[3][r];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < AMAX; ++k)
-        if (k < a.A) acc[po.Wo + k * H + ftrue] += gWo[k];
-      acc[po.Wv + ftrue] += gWv;
-      if (lane < a.A) acc[po.bo + lane] += gbh;
-      if (lane == 32) acc[po.bv] += gbh;
-      if (CONT && lane >= 33 && lane < 33 + a.A) acc[po.ls + (lane - 33)] += gbh;
-      if (lane == 0) {
-        acc[a.p_total + 0] += s_pi;
-        acc[a.p_total + 1] += s_v;
-        acc[a.p_total + 2] += s_ent;
-      }
+    for (int ib = 0; ib < 4; ++ib) {
+      const int i = 16 * ib + l15;
+      slab[po.W2 + o * H + i] = gW2[ib][r];
+      slab[po.Wa + o * H + i] = gWa[ib][r];
+      slab[po.Wc + o * H + i] = gWc[ib][r];
     }
-    __syncthreads();
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      const int i = 16 * ib + l15;
+      if (i < a.D) slab[po.W1 + o * a.D + i] = gW1[ib][r];
+    }
+    if (l15 == 0) {
+      slab[po.b1 + o] = gb[0][r];
+      slab[po.b2 + o] = gb[1][r];
+      slab[po.ba + o] = gb[2][r];
+      slab[po.bc + o] = gb[3][r];
+    }
   }
-  float* slab = a.slabs + (int64_t)blockIdx.x * a.slab_stride;
-  for (int k = tid; k < np; k += kThreads) slab[k] = acc[k];
+  // head partials: [wave][AMAX + 2 (Wv, bias/log-std column sums) + 1 (loss)][64] in LDS
+  constexpr int NH = AMAX + 3;
+  __syncthreads();  // all waves are done with the step images
+  float* hp = lds_ + wave * NH * 64;
+#pragma unroll
+  for (int k = 0; k < AMAX; ++k) hp[k * 64 + lane] = gWo[k];
+  hp[AMAX * 64 + lane] = gWv;
+  hp[(AMAX + 1) * 64 + lane] = gbh;
+  hp[(AMAX + 2) * 64 + lane] = lane == 0 ? s_pi : (lane == 1 ? s_v : (lane == 2 ? s_ent : 0.f));
+  __syncthreads();
+  const int fcol = lane;  // permuted feature column held by this lane
+  const int c15 = fcol & 15;
+  const int ftrue = (fcol & ~15) + 4 * (c15 & 3) + (c15 >> 2);
+  for (int e = wave; e < NH; e += kThreads / 64) {
+    const float v = ((lds_[0 * NH * 64 + e * 64 + lane] + lds_[1 * NH * 64 + e * 64 + lane]) +
+                     lds_[2 * NH * 64 + e * 64 + lane]) + lds_[3 * NH * 64 + e * 64 + lane];
+    if (e < AMAX) {
+      if (e < a.A) slab[po.Wo + e * H + ftrue] = v;
+    } else if (e == AMAX) {
+      slab[po.Wv + ftrue] = v;
+    } else if (e == AMAX + 1) {
+      if (lane < a.A) slab[po.bo + lane] = v;
+      if (lane == 32) slab[po.bv] = v;
+      if (CONT && lane >= 33 && lane < 33 + a.A) slab[po.ls + (lane - 33)] = v;
+    } else {
+      if (lane < 3) slab[a.p_total + lane] = v;
+    }
+  }
 }
 
 }  // namespace

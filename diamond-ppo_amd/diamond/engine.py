@@ -18,6 +18,7 @@ Two paths, chosen once per agent:
 from __future__ import annotations
 
 import ctypes
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -205,6 +206,9 @@ class NativeLearner:
         if self.world > 1:
             self._init_comm()
         self.last_trace = None
+        # host-side seconds per phase of learn() (permutation staging wait, exact NumPy-RNG
+        # permutations, kernel enqueue) -- reported by bench.py
+        self.host_seconds = {"perm_wait": 0.0, "perms": 0.0, "enqueue": 0.0, "calls": 0}
 
     def _init_comm(self):
         d = torch.distributed
@@ -236,14 +240,23 @@ class NativeLearner:
         ro.check(self.T, self.N, self.D, self.A, self.continuous)
         step0 = adam_step_count(self.optimizer, self.flat)
         if self.fused:
+            t0 = time.perf_counter()
             stream = torch.cuda.current_stream(self.device).cuda_stream
             pinned = self.handle.perm_buffer()
+            t1 = time.perf_counter()
             self.draw_permutations(pinned)
+            t2 = time.perf_counter()
             hp = hparams(cfg, lr, step0)
             N.check(self.handle.lib.dppo_learn_f32(
                 self.handle.h, ctypes.byref(ro.as_struct()), self.flat.flat.data_ptr(),
                 self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
                 ctypes.byref(outputs) if outputs is not None else None, stream), "dppo_learn_f32")
+            t3 = time.perf_counter()
+            hs = self.host_seconds
+            hs["perm_wait"] += t1 - t0
+            hs["perms"] += t2 - t1
+            hs["enqueue"] += t3 - t2
+            hs["calls"] += 1
         else:
             self._learn_generic(ro, lr, step0)
         advance_adam_steps(self.optimizer, self.flat, cfg.num_epochs * cfg.num_minibatches)
