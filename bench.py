@@ -214,9 +214,10 @@ def main():
     h = agent._learner.handle
     h.set_timing(True)
     hs = agent._learner.host_seconds
-    for k in ("perm_wait", "perms", "enqueue"):
+    for k in ("perms", "enqueue", "draft_start"):
         hs[k] = 0.0
     hs["calls"] = 0
+    hs["lookahead_hits"] = 0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -298,7 +299,8 @@ def main():
             "kernels": kernel_ms,
             "device_ms_per_step": round(dev_ms / args.steps, 4),
             "host_ms_per_step": {k: round(hs[k] / max(hs["calls"], 1) * 1e3, 4)
-                                 for k in ("perm_wait", "perms", "enqueue")},
+                                 for k in ("perms", "enqueue", "draft_start")},
+            "perm_lookahead_hits": hs["lookahead_hits"],
             "final_loss": float(loss_trace[-1, 0]),
             "device": {"name": torch.cuda.get_device_name(device),
                        "arch": getattr(torch.cuda.get_device_properties(device), "gcnArchName", ""),

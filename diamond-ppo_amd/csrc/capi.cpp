@@ -73,10 +73,13 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
-  int32_t* perms_dev = nullptr;
-  int32_t* perms_pinned = nullptr;
-  hipEvent_t perm_copy_done = nullptr;
-  bool perm_copy_pending = false;
+  int32_t* perms_dev = nullptr;     // [E][B] permutations the minibatch kernels gather with
+  int32_t* targets_dev = nullptr;   // [E][B] Fisher-Yates targets (dppo_learn_targets_f32)
+  int32_t* perm_scratch = nullptr;  // [3][E][B] Fisher-Yates resolution scratch
+  // two pinned host staging slots, each with the event that marks its upload done
+  int32_t* perms_pinned[2] = {nullptr, nullptr};
+  hipEvent_t perm_copy_done[2] = {nullptr, nullptr};
+  bool perm_copy_pending[2] = {false, false};
   int32_t trace_rows = 0;
   hipStream_t last_stream = nullptr;
   // optional per-kernel-class timing with HIP events on the launch stream
@@ -178,7 +181,9 @@ int dalloc(T** p, int64_t n) {
 
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
-enum KClass { K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_NCLASS };
+enum KClass {
+  K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_PERM, K_NCLASS
+};
 
 hipEvent_t pool_event(dppo_handle* h) {
   if (h->pool_used == h->pool.size()) {
@@ -336,6 +341,86 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int3
 
 }  // namespace
 
+namespace {
+
+// Upload the host [E][B] buffer (permutations or Fisher-Yates targets) to `dst`, stream-ordered.
+// A pinned slot is copied from directly (pure DMA); any other buffer is first staged in slot 0.
+int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, hipStream_t s) {
+  const size_t pbytes = (size_t)(h->dims.num_epochs * h->B) * sizeof(int32_t);
+  int slot = host == h->perms_pinned[1] ? 1 : 0;
+  if (host != h->perms_pinned[slot]) {
+    if (h->perm_copy_pending[0]) DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done[0]));
+    std::memcpy(h->perms_pinned[0], host, pbytes);
+  }
+  DPPO_HIP_CHECK(
+      hipMemcpyAsync(dst, h->perms_pinned[slot], pbytes, hipMemcpyHostToDevice, s));
+  DPPO_HIP_CHECK(hipEventRecord(h->perm_copy_done[slot], s));
+  h->perm_copy_pending[slot] = true;
+  return DPPO_OK;
+}
+
+int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float* adam_m,
+               float* adam_v, const dppo_hparams* hp, const int32_t* host_buf, bool targets,
+               const dppo_learn_outputs* outputs, void* stream) {
+  if (!h || !params || !adam_m || !adam_v || !hp || !host_buf) {
+    set_error("null argument to dppo_learn_f32");
+    return DPPO_EINVAL;
+  }
+  const dppo_dims& d = h->dims;
+  if (h->B % d.num_minibatches != 0) {
+    // the reference's perms.reshape(E, M, B // M) raises ValueError (ppo.py:255)
+    set_error("cannot reshape array of size %lld into shape (%d,%d,%lld)",
+              (long long)(h->B * d.num_epochs), d.num_epochs, d.num_minibatches,
+              (long long)(h->B / d.num_minibatches));
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t s = S(stream);
+  const int64_t E = d.num_epochs, M = d.num_minibatches;
+  // permutations (ppo.py:252-255): host -> pinned staging -> device, stream-ordered; given as
+  // swap targets they are shuffled on the device while nothing else depends on them yet
+  if (targets) {
+    DPPO_TRY(upload_perms(h, host_buf, h->targets_dev, s));
+    Timed tm(h, K_PERM, s);
+    DPPO_TRY(launch_perm_resolve(h->targets_dev, h->perms_dev, h->B, (int32_t)E, h->perm_scratch,
+                                 s));
+  } else {
+    DPPO_TRY(upload_perms(h, host_buf, h->perms_dev, s));
+  }
+  DPPO_TRY(prepare(h, rollout, params, hp, outputs, s));
+  // (6) E x M dependent optimizer steps (ppo.py:258-285)
+  const int32_t mb = h->mb;
+  const int32_t m_total = mb * (h->comm ? h->nranks : 1);
+  const float inv_m = (float)(1.0 / (double)m_total);
+  for (int64_t e = 0; e < E; ++e) {
+    for (int64_t j = 0; j < M; ++j) {
+      const int64_t k = e * M + j;
+      const int32_t* idx = h->perms_dev + e * h->B + j * mb;
+      DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
+      const double step = (double)(hp->adam_step + k + 1);
+      const double bc1 = 1.0 - std::pow((double)hp->adam_beta1, step);
+      const double bc2 = 1.0 - std::pow((double)hp->adam_beta2, step);
+      const double step_size = hp->lr / bc1;
+      const double bc2_sqrt = std::pow(bc2, 0.5);
+      Timed tm(h, K_ADAM, s);
+      // single device: the norm comes from the reduce kernel's per-block partials; after an
+      // all-reduce those are stale, so the Adam kernel recomputes it from the gradient
+      const bool multi = h->comm && h->nranks > 1;
+      DPPO_TRY(launch_clip_adam_traced(params, h->grad, adam_m, adam_v, h->layout.total,
+                                       multi ? nullptr : h->sq_part,
+                                       slab_reduce_blocks(h->layout.total), hp->grad_norm_clip,
+                                       (float)(-step_size),
+                                       (float)bc2_sqrt, hp->adam_beta1, hp->adam_beta2,
+                                       hp->adam_eps, nullptr, h->trace + k * DPPO_TRACE_FIELDS,
+                                       inv_m, hp->value_loss_weight, hp->entropy_beta, s));
+    }
+  }
+  h->last_stream = s;
+  return DPPO_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* dppo_version(void) { return "libdppo 0.1.0 (gfx950)"; }
@@ -408,18 +493,19 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
   chk(dalloc(&h->perms_dev, E * h->B));
-  if (rc == DPPO_OK) {
-    hipError_t e = hipHostMalloc((void**)&h->perms_pinned, (size_t)(E * h->B) * sizeof(int32_t),
-                                 hipHostMallocDefault);
+  chk(dalloc(&h->targets_dev, E * h->B));
+  chk(dalloc(&h->perm_scratch, 3 * E * h->B));
+  for (int k = 0; k < 2 && rc == DPPO_OK; ++k) {
+    hipError_t e = hipHostMalloc((void**)&h->perms_pinned[k],
+                                 (size_t)(E * h->B) * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
       set_error("hipHostMalloc failed: %s", hipGetErrorString(e));
       rc = DPPO_ENOMEM;
+    } else if (hipEventCreateWithFlags(&h->perm_copy_done[k], hipEventDisableTiming) !=
+               hipSuccess) {
+      set_error("hipEventCreate failed");
+      rc = DPPO_EHIP;
     }
-  }
-  if (rc == DPPO_OK && hipEventCreateWithFlags(&h->perm_copy_done, hipEventDisableTiming) !=
-                           hipSuccess) {
-    set_error("hipEventCreate failed");
-    rc = DPPO_EHIP;
   }
   if (rc == DPPO_OK) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
@@ -455,8 +541,12 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->dsum);
   (void)hipFree(h->sq_part);
   (void)hipFree(h->perms_dev);
-  if (h->perms_pinned) (void)hipHostFree(h->perms_pinned);
-  if (h->perm_copy_done) (void)hipEventDestroy(h->perm_copy_done);
+  (void)hipFree(h->targets_dev);
+  (void)hipFree(h->perm_scratch);
+  for (int k = 0; k < 2; ++k) {
+    if (h->perms_pinned[k]) (void)hipHostFree(h->perms_pinned[k]);
+    if (h->perm_copy_done[k]) (void)hipEventDestroy(h->perm_copy_done[k]);
+  }
   for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
   delete h;
 }
@@ -562,76 +652,40 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
                           (float)bc2_sqrt, beta1, beta2, eps, out_norm, S(stream));
 }
 
+
 int dppo_learn_f32(dppo_handle* h, const dppo_rollout* rollout, float* params, float* adam_m,
                    float* adam_v, const dppo_hparams* hp, const int32_t* host_perms,
                    const dppo_learn_outputs* outputs, void* stream) {
-  if (!h || !params || !adam_m || !adam_v || !hp || !host_perms) {
-    set_error("null argument to dppo_learn_f32");
-    return DPPO_EINVAL;
-  }
-  const dppo_dims& d = h->dims;
-  if (h->B % d.num_minibatches != 0) {
-    // the reference's perms.reshape(E, M, B // M) raises ValueError (ppo.py:255)
-    set_error("cannot reshape array of size %lld into shape (%d,%d,%lld)",
-              (long long)(h->B * d.num_epochs), d.num_epochs, d.num_minibatches,
-              (long long)(h->B / d.num_minibatches));
-    return DPPO_EINVAL;
-  }
-  DPPO_HIP_CHECK(hipSetDevice(h->device));
-  hipStream_t s = S(stream);
-  DPPO_TRY(prepare(h, rollout, params, hp, outputs, s));
-  // permutations: host -> pinned staging -> device, stream-ordered (ppo.py:252-255)
-  const int64_t E = d.num_epochs, M = d.num_minibatches;
-  const size_t pbytes = (size_t)(E * h->B) * sizeof(int32_t);
-  if (host_perms != h->perms_pinned) {
-    if (h->perm_copy_pending) DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done));
-    std::memcpy(h->perms_pinned, host_perms, pbytes);
-  }
-  DPPO_HIP_CHECK(hipMemcpyAsync(h->perms_dev, h->perms_pinned, pbytes, hipMemcpyHostToDevice, s));
-  DPPO_HIP_CHECK(hipEventRecord(h->perm_copy_done, s));
-  h->perm_copy_pending = true;
-  // (6) E x M dependent optimizer steps (ppo.py:258-285)
-  const int32_t mb = h->mb;
-  const int32_t m_total = mb * (h->comm ? h->nranks : 1);
-  const float inv_m = (float)(1.0 / (double)m_total);
-  for (int64_t e = 0; e < E; ++e) {
-    for (int64_t j = 0; j < M; ++j) {
-      const int64_t k = e * M + j;
-      const int32_t* idx = h->perms_dev + e * h->B + j * mb;
-      DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
-      const double step = (double)(hp->adam_step + k + 1);
-      const double bc1 = 1.0 - std::pow((double)hp->adam_beta1, step);
-      const double bc2 = 1.0 - std::pow((double)hp->adam_beta2, step);
-      const double step_size = hp->lr / bc1;
-      const double bc2_sqrt = std::pow(bc2, 0.5);
-      Timed tm(h, K_ADAM, s);
-      // single device: the norm comes from the reduce kernel's per-block partials; after an
-      // all-reduce those are stale, so the Adam kernel recomputes it from the gradient
-      const bool multi = h->comm && h->nranks > 1;
-      DPPO_TRY(launch_clip_adam_traced(params, h->grad, adam_m, adam_v, h->layout.total,
-                                       multi ? nullptr : h->sq_part,
-                                       slab_reduce_blocks(h->layout.total), hp->grad_norm_clip,
-                                       (float)(-step_size),
-                                       (float)bc2_sqrt, hp->adam_beta1, hp->adam_beta2,
-                                       hp->adam_eps, nullptr, h->trace + k * DPPO_TRACE_FIELDS,
-                                       inv_m, hp->value_loss_weight, hp->entropy_beta, s));
-    }
-  }
-  h->last_stream = s;
-  return DPPO_OK;
+  return learn_impl(h, rollout, params, adam_m, adam_v, hp, host_perms, false, outputs, stream);
 }
 
-int dppo_perm_buffer(dppo_handle* h, int32_t** out) {
-  if (!h || !out) {
-    set_error("null argument to dppo_perm_buffer");
+int dppo_learn_targets_f32(dppo_handle* h, const dppo_rollout* rollout, float* params,
+                           float* adam_m, float* adam_v, const dppo_hparams* hp,
+                           const int32_t* host_targets, const dppo_learn_outputs* outputs,
+                           void* stream) {
+  return learn_impl(h, rollout, params, adam_m, adam_v, hp, host_targets, true, outputs, stream);
+}
+
+int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
+                      int32_t* scratch, void* stream) {
+  if (!targets || !perms || !scratch || n < 0 || n > 0x7FFFFFFF || count < 0) {
+    set_error("invalid argument to dppo_perm_resolve");
+    return DPPO_EINVAL;
+  }
+  return launch_perm_resolve(targets, perms, n, count, scratch, S(stream));
+}
+
+int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out) {
+  if (!h || !out || slot < 0 || slot > 1) {
+    set_error("invalid argument to dppo_perm_buffer");
     return DPPO_EINVAL;
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
-  if (h->perm_copy_pending) {
-    DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done));
-    h->perm_copy_pending = false;
+  if (h->perm_copy_pending[slot]) {
+    DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done[slot]));
+    h->perm_copy_pending[slot] = false;
   }
-  *out = h->perms_pinned;
+  *out = h->perms_pinned[slot];
   return DPPO_OK;
 }
 

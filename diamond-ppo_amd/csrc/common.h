@@ -100,4 +100,9 @@ int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, 
                      float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
                      float* out_norm, hipStream_t s);
 
+// Fisher-Yates resolution (shuffle.hip): perms[c][n] from swap targets[c][n];
+// scratch = 3 * count * n int32.
+int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
+                        int32_t* scratch, hipStream_t s);
+
 }  // namespace dppo

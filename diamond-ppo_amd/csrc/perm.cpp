@@ -12,6 +12,8 @@
 //
 // Throughput: the twist is written so the compiler vectorises it; the draw/accept loop is
 // branch-light; the swap runs on a 4-byte array (2 MiB at B = 524,288 fits in L2).
+// dppo_perm_targets_numpy stops after the draws: the swaps are resolved on the GPU instead
+// (shuffle.hip), which takes the sequential swap chain off the host's critical path.
 
 #include <cstdint>
 #include <cstring>
@@ -26,35 +28,36 @@ constexpr uint32_t kMatrixA = 0x9908B0DFu;
 constexpr uint32_t kUpper = 0x80000000u;
 constexpr uint32_t kLower = 0x7FFFFFFFu;
 
+// One MT19937 block: twist the 624-word state and temper it into out[].  The three twist
+// ranges only depend on words at distance >= 227 (or the block before), so each loop
+// vectorises; AVX2 clones are picked at load time where the host has them.
+__attribute__((target_clones("avx2", "default"))) void twist_block(uint32_t* __restrict mt,
+                                                                   uint32_t* __restrict out) {
+  int i = 0;
+  for (; i < kN - kM; ++i) {
+    uint32_t y = (mt[i] & kUpper) | (mt[i + 1] & kLower);
+    mt[i] = mt[i + kM] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+  }
+  for (; i < kN - 1; ++i) {
+    uint32_t y = (mt[i] & kUpper) | (mt[i + 1] & kLower);
+    mt[i] = mt[i + (kM - kN)] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+  }
+  uint32_t y = (mt[kN - 1] & kUpper) | (mt[0] & kLower);
+  mt[kN - 1] = mt[kM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
+  for (int k = 0; k < kN; ++k) {
+    uint32_t t = mt[k];
+    t ^= t >> 11;
+    t ^= (t << 7) & 0x9D2C5680u;
+    t ^= (t << 15) & 0xEFC60000u;
+    t ^= t >> 18;
+    out[k] = t;
+  }
+}
+
 struct MT {
   uint32_t mt[kN];
-  int pos;
-  uint32_t out[kN];  // tempered outputs of the current twist
-  int opos;          // next index into out[]
-
-  void twist() {
-    int i = 0;
-    for (; i < kN - kM; ++i) {
-      uint32_t y = (mt[i] & kUpper) | (mt[i + 1] & kLower);
-      mt[i] = mt[i + kM] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
-    }
-    for (; i < kN - 1; ++i) {
-      uint32_t y = (mt[i] & kUpper) | (mt[i + 1] & kLower);
-      mt[i] = mt[i + (kM - kN)] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
-    }
-    uint32_t y = (mt[kN - 1] & kUpper) | (mt[0] & kLower);
-    mt[kN - 1] = mt[kM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & kMatrixA);
-    for (int k = 0; k < kN; ++k) {
-      uint32_t t = mt[k];
-      t ^= t >> 11;
-      t ^= (t << 7) & 0x9D2C5680u;
-      t ^= (t << 15) & 0xEFC60000u;
-      t ^= t >> 18;
-      out[k] = t;
-    }
-    pos = 0;
-    opos = 0;
-  }
+  uint32_t out[kN];  // tempered outputs of the current block
+  int pos;           // next unconsumed word of the block (numpy's `pos`)
 
   void load(const uint32_t* key, int p) {
     std::memcpy(mt, key, sizeof(mt));
@@ -68,13 +71,6 @@ struct MT {
       t ^= t >> 18;
       out[k] = t;
     }
-    opos = p;
-  }
-
-  inline uint32_t next32() {
-    if (opos >= kN) twist();
-    ++pos;
-    return out[opos++];
   }
 };
 
@@ -87,39 +83,81 @@ inline uint32_t smear(uint32_t m) {
   return m;
 }
 
+// Fisher-Yates targets of `count` successive permutations of arange(n): j[c][i] for
+// i = n-1 .. 1 (j[c][0] = 0), the draw/accept state machine of numpy's random_interval with the
+// accept step branch-free (the draw is always stored; i only advances on acceptance).
+// Within one mask band [lo, i] the loop runs min(words left in the block, i - lo + 1) draws
+// with no exit test: i falls by at most one per draw, so it cannot leave the band early.
+void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
+  int opos = g.pos;
+  for (int32_t c = 0; c < count; ++c) {
+    int32_t* __restrict j = out + (int64_t)c * n;
+    if (n > 0) j[0] = 0;
+    uint32_t i = n > 0 ? (uint32_t)(n - 1) : 0u;
+    while (i >= 1) {
+      const uint32_t mask = smear(i);
+      const uint32_t lo = (mask >> 1) + 1;  // all draws in [lo, i] share this mask
+      while (i >= lo) {
+        if (opos >= kN) {
+          twist_block(g.mt, g.out);
+          opos = 0;
+        }
+        const uint32_t* __restrict o = g.out + opos;
+        const uint32_t left = (uint32_t)(kN - opos);
+        const uint32_t run = left < i - lo + 1 ? left : i - lo + 1;
+        for (uint32_t k = 0; k < run; ++k) {
+          const uint32_t v = o[k] & mask;
+          j[i] = (int32_t)v;
+          // accept (v <= i): i - 1; reject: i.  cmp sets CF = (i < v), adc adds CF - 1: a
+          // 2-cycle loop-carried chain instead of the compiler's cmp/setcc/movzx/sub
+#if defined(__x86_64__)
+          asm("cmpl %1, %0\n\tadcl $-1, %0" : "+r"(i) : "r"(v) : "cc");
+#else
+          i = i - 1u + (i < v ? 1u : 0u);
+#endif
+        }
+        opos += (int)run;
+      }
+    }
+  }
+  g.pos = opos;
+}
+
+bool bad_args(const uint32_t* key, const int32_t* pos, int64_t n, int32_t count,
+              const int32_t* out) {
+  return !key || !pos || !out || n < 0 || n > 0x7FFFFFFF || count < 0 || *pos < 0 || *pos > kN;
+}
+
 }  // namespace
+
+extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
+                                       int32_t* out) {
+  if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
+  MT g;
+  g.load(key, *pos);
+  draw_targets(g, n, count, out);
+  std::memcpy(key, g.mt, sizeof(g.mt));
+  *pos = g.pos;
+  return DPPO_OK;
+}
 
 extern "C" int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
                                int32_t* out) {
-  if (!key || !pos || !out || n < 0 || n > 0x7FFFFFFF || count < 0 || *pos < 0 || *pos > kN)
-    return DPPO_EINVAL;
+  if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
   MT g;
   g.load(key, *pos);
-  // Pass 1 draws the Fisher-Yates targets j[i] with a branch-free accept step (the draw is
-  // always stored; i only advances on acceptance), pass 2 applies the swaps with the target
-  // lines prefetched ahead -- the two passes are the same state machine as numpy's fused loop.
-  uint32_t* j = new uint32_t[n > 1 ? n : 1];
+  // targets first (into out itself), then the swaps in place with the target lines prefetched
+  // ahead -- the same state machine as numpy's fused loop
+  draw_targets(g, n, count, out);
+  int32_t* j = new int32_t[n > 1 ? n : 1];
   for (int32_t c = 0; c < count; ++c) {
     int32_t* a = out + (int64_t)c * n;
+    std::memcpy(j, a, (size_t)n * sizeof(int32_t));
     for (int64_t k = 0; k < n; ++k) a[k] = (int32_t)k;
-    int64_t i = n - 1;
-    while (i >= 1) {
-      const uint32_t mx = (uint32_t)i;
-      const uint32_t mask = smear(mx);
-      // all draws in [lo, i] share this mask
-      const int64_t lo = (int64_t)((mask >> 1) + 1) > 1 ? (int64_t)((mask >> 1) + 1) : 1;
-      while (i >= lo) {
-        if (g.opos >= kN) g.twist();
-        const uint32_t v = g.out[g.opos++] & mask;
-        ++g.pos;
-        j[i] = v;
-        i -= (v <= (uint32_t)i) ? 1 : 0;
-      }
-    }
     constexpr int kAhead = 16;
     for (int64_t k = n - 1; k >= 1; --k) {
       if (k - kAhead >= 1) __builtin_prefetch(a + j[k - kAhead], 1, 3);
-      const uint32_t v = j[k];
+      const int32_t v = j[k];
       const int32_t t = a[k];
       a[k] = a[v];
       a[v] = t;

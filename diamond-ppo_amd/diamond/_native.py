@@ -27,9 +27,11 @@ EXPORTED = [
     "dppo_gae_f32", "dppo_adv_stats", "dppo_adv_normalize_f32", "dppo_old_policy_f32",
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
-    "dppo_comm_init", "dppo_set_timing", "dppo_get_timing",
+    "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
+    "dppo_perm_targets_numpy", "dppo_perm_resolve",
 ]
-TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam", "allreduce"]
+TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
+                  "allreduce", "perm"]
 
 
 class Dims(ctypes.Structure):
@@ -94,13 +96,17 @@ def load():
         "dppo_old_policy_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
         "dppo_learn_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,
                                           P(LearnOutputs), vp]),
+        "dppo_learn_targets_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,
+                                                  P(LearnOutputs), vp]),
         "dppo_minibatch_grad_f32": (ctypes.c_int, [vp, vp, vp, i32, i32, P(HParams), vp, vp, vp]),
         "dppo_prepare_f32": (ctypes.c_int, [vp, P(Rollout), vp, P(HParams), P(LearnOutputs), vp]),
         "dppo_clip_adam_f32": (ctypes.c_int, [vp, vp, vp, vp, i64, f32, f64, f32, f32, f32, i64,
                                               vp, vp]),
-        "dppo_perm_buffer": (ctypes.c_int, [vp, P(vp)]),
+        "dppo_perm_buffer": (ctypes.c_int, [vp, i32, P(vp)]),
         "dppo_get_trace": (ctypes.c_int, [vp, vp, i32]),
         "dppo_perm_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
+        "dppo_perm_targets_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
+        "dppo_perm_resolve": (ctypes.c_int, [vp, vp, i64, i32, vp, vp]),
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
         "dppo_set_timing": (ctypes.c_int, [vp, i32]),
@@ -148,33 +154,60 @@ def param_layout(dims: Dims) -> Layout:
     return L
 
 
-def perm_numpy(key: np.ndarray, pos: int, n: int, count: int, out: np.ndarray | int) -> int:
-    """NumPy-legacy-exact permutations (host C++).  ``key`` (uint32[624]) is advanced in place;
-    returns the new ``pos``.  ``out`` is an int32 array of count*n or a raw host address."""
+def _mt_call(fn: str, key: np.ndarray, pos: int, n: int, count: int, out) -> int:
     assert key.dtype == np.uint32 and key.size == 624 and key.flags.c_contiguous
     p = ctypes.c_int32(int(pos))
     dst = out if isinstance(out, int) else out.ctypes.data
     if not isinstance(out, int):
         assert out.dtype == np.int32 and out.size >= n * count and out.flags.c_contiguous
-    check(load().dppo_perm_numpy(key.ctypes.data, ctypes.byref(p), int(n), int(count), dst),
-          "dppo_perm_numpy")
+    check(getattr(load(), fn)(key.ctypes.data, ctypes.byref(p), int(n), int(count), dst), fn)
     return int(p.value)
+
+
+def perm_numpy(key: np.ndarray, pos: int, n: int, count: int, out: np.ndarray | int) -> int:
+    """NumPy-legacy-exact permutations (host C++).  ``key`` (uint32[624]) is advanced in place;
+    returns the new ``pos``.  ``out`` is an int32 array of count*n or a raw host address."""
+    return _mt_call("dppo_perm_numpy", key, pos, n, count, out)
+
+
+def perm_targets_numpy(key: np.ndarray, pos: int, n: int, count: int,
+                       out: np.ndarray | int) -> int:
+    """The MT19937 half of :func:`perm_numpy`: Fisher-Yates swap targets ``out[c][i] = j_i``
+    (the device resolves the swaps).  Advances ``key``/``pos`` exactly like perm_numpy."""
+    return _mt_call("dppo_perm_targets_numpy", key, pos, n, count, out)
+
+
+def mt_state(rng=None):
+    """(key copy, pos, full state tuple) of the global legacy NumPy RNG (or ``rng``)."""
+    st = (np.random.get_state() if rng is None else rng.get_state())
+    if st[0] != "MT19937":
+        raise ValueError("only the legacy MT19937 RandomState is supported")
+    return np.array(st[1], dtype=np.uint32, copy=True), int(st[2]), st
+
+
+def set_mt_state(st, key: np.ndarray, pos: int, rng=None):
+    new = (st[0], key, pos, st[3], st[4])
+    if rng is None:
+        np.random.set_state(new)
+    else:
+        rng.set_state(new)
 
 
 def numpy_rng_permutations(n: int, count: int, out, rng=None):
     """Draw ``count`` permutations of range(n) exactly as ``count`` calls of
     ``rng.permutation(n)`` would (rng = the global legacy NumPy RNG by default, reference
     ppo.py:254), leaving the RNG in the same final state."""
-    st = (np.random.get_state() if rng is None else rng.get_state())
-    if st[0] != "MT19937":
-        raise ValueError("only the legacy MT19937 RandomState is supported")
-    key = np.array(st[1], dtype=np.uint32, copy=True)
-    pos = perm_numpy(key, int(st[2]), n, count, out)
-    new = (st[0], key, pos, st[3], st[4])
-    if rng is None:
-        np.random.set_state(new)
-    else:
-        rng.set_state(new)
+    key, pos, st = mt_state(rng)
+    pos = perm_numpy(key, pos, n, count, out)
+    set_mt_state(st, key, pos, rng)
+
+
+def perm_resolve(targets_dev: int, perms_dev: int, n: int, count: int, scratch_dev: int,
+                 stream: int):
+    """Device Fisher-Yates resolution (dppo_perm_resolve): perms[c] = arange(n) shuffled by
+    targets[c]; scratch holds 3*count*n int32."""
+    check(load().dppo_perm_resolve(targets_dev, perms_dev, int(n), int(count), scratch_dev,
+                                   stream), "dppo_perm_resolve")
 
 
 class Handle:
@@ -200,9 +233,10 @@ class Handle:
         except Exception:
             pass
 
-    def perm_buffer(self) -> int:
+    def perm_buffer(self, slot: int = 0) -> int:
+        """Pinned [E][B] int32 staging slot 0/1 (waits for its previous upload)."""
         p = ctypes.c_void_p()
-        check(self.lib.dppo_perm_buffer(self.h, ctypes.byref(p)), "dppo_perm_buffer")
+        check(self.lib.dppo_perm_buffer(self.h, int(slot), ctypes.byref(p)), "dppo_perm_buffer")
         return p.value
 
     def trace(self, rows: int) -> np.ndarray:

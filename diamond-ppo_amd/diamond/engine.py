@@ -6,6 +6,13 @@ Adam buffers the gfx950 kernels update in place, keeps the reference's ``nn.Modu
 ``LinearLR`` behave exactly as in the reference), draws the minibatch permutations from the global
 NumPy RNG bit-exactly, and issues ONE native call per learn().
 
+Permutations (ppo.py:252-254) are split in two: the host runs NumPy's MT19937 draws (the
+Fisher-Yates swap targets, ``dppo_perm_targets_numpy``), the device resolves the swaps
+(``shuffle.hip``).  The draws for learn k+1 start on a host thread as soon as learn k is
+enqueued, from the RNG state learn k leaves behind; learn k+1 uses them only if the global NumPy
+RNG still holds exactly that state (otherwise it draws afresh), so the results and the RNG stream
+stay bit-identical to the reference's.
+
 Two paths, chosen once per agent:
 
 * **fused** -- default network at supported sizes (hidden 64, obs_dim <= 32, actions <= 16):
@@ -18,6 +25,8 @@ Two paths, chosen once per agent:
 from __future__ import annotations
 
 import ctypes
+import os
+import threading
 import time
 from dataclasses import dataclass
 
@@ -206,9 +215,13 @@ class NativeLearner:
         if self.world > 1:
             self._init_comm()
         self.last_trace = None
-        # host-side seconds per phase of learn() (permutation staging wait, exact NumPy-RNG
-        # permutations, kernel enqueue) -- reported by bench.py
-        self.host_seconds = {"perm_wait": 0.0, "perms": 0.0, "enqueue": 0.0, "calls": 0}
+        # host-side seconds per phase of learn() (swap targets incl. waiting for the look-ahead
+        # draft, native enqueue, starting the next draft) -- reported by bench.py
+        self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "calls": 0,
+                             "lookahead_hits": 0}
+        self.lookahead = os.environ.get("DPPO_PERM_LOOKAHEAD", "1") != "0"
+        self._draft = None
+        self._slot = 0
 
     def _init_comm(self):
         d = torch.distributed
@@ -224,11 +237,39 @@ class NativeLearner:
             self.flat.flat.copy_(cpu)
 
     # -----------------------------------------------------------------------------------------
-    def draw_permutations(self, out_addr: int):
-        """np.random.permutation(B) for each epoch (ppo.py:252-254), bit-exact, written into the
-        pinned staging buffer at ``out_addr`` (one contiguous [E][B] int32 block)."""
-        B = self.T * self.N
-        N.numpy_rng_permutations(B, self.cfg.num_epochs, out_addr)
+    def _start_draft(self, key: np.ndarray, pos: int):
+        """Draw the next learn's swap targets on a host thread (ctypes releases the GIL)."""
+        slot = 1 - self._slot
+        buf = self.handle.perm_buffer(slot)
+        d = {"slot": slot, "buf": buf, "key_in": key.copy(), "pos_in": pos, "ok": False}
+
+        def work():
+            k = d["key_in"].copy()
+            d["pos_out"] = N.perm_targets_numpy(k, d["pos_in"], self.T * self.N,
+                                                self.cfg.num_epochs, buf)
+            d["key_out"] = k
+            d["ok"] = True
+
+        d["thread"] = threading.Thread(target=work, name="dppo-perm-draft", daemon=True)
+        d["thread"].start()
+        self._draft = d
+
+    def _targets(self):
+        """This learn's swap targets in a pinned slot; advances the global NumPy RNG exactly as
+        num_epochs calls of np.random.permutation(B) would (ppo.py:254)."""
+        key, pos, st = N.mt_state()
+        d, self._draft = self._draft, None
+        if d is not None:
+            d["thread"].join()
+            if d["ok"] and d["pos_in"] == pos and np.array_equal(d["key_in"], key):
+                self._slot = d["slot"]
+                N.set_mt_state(st, d["key_out"], d["pos_out"])
+                self.host_seconds["lookahead_hits"] += 1
+                return d["buf"], d["key_out"], d["pos_out"]
+        buf = self.handle.perm_buffer(self._slot)
+        pos = N.perm_targets_numpy(key, pos, self.T * self.N, self.cfg.num_epochs, buf)
+        N.set_mt_state(st, key, pos)
+        return buf, key, pos
 
     def learn(self, ro: DeviceRollout, lr: float, outputs: N.LearnOutputs | None = None):
         cfg = self.cfg
@@ -242,19 +283,22 @@ class NativeLearner:
         if self.fused:
             t0 = time.perf_counter()
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            pinned = self.handle.perm_buffer()
+            pinned, key, pos = self._targets()
             t1 = time.perf_counter()
-            self.draw_permutations(pinned)
+            # the next learn's draws overlap this learn's enqueue and device time
+            if self.lookahead:
+                self._start_draft(key, pos)
             t2 = time.perf_counter()
             hp = hparams(cfg, lr, step0)
-            N.check(self.handle.lib.dppo_learn_f32(
+            N.check(self.handle.lib.dppo_learn_targets_f32(
                 self.handle.h, ctypes.byref(ro.as_struct()), self.flat.flat.data_ptr(),
                 self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
-                ctypes.byref(outputs) if outputs is not None else None, stream), "dppo_learn_f32")
+                ctypes.byref(outputs) if outputs is not None else None, stream),
+                "dppo_learn_targets_f32")
             t3 = time.perf_counter()
             hs = self.host_seconds
-            hs["perm_wait"] += t1 - t0
-            hs["perms"] += t2 - t1
+            hs["perms"] += t1 - t0
+            hs["draft_start"] += t2 - t1
             hs["enqueue"] += t3 - t2
             hs["calls"] += 1
         else:

@@ -29,6 +29,9 @@
 extern "C" {
 #endif
 
+/* the library is built with -fvisibility=hidden: only these declarations are exported */
+#pragma GCC visibility push(default)
+
 #define DPPO_OK 0
 #define DPPO_EINVAL (-1)       /* invalid argument (Python: ValueError / AssertionError) */
 #define DPPO_EHIP (-2)         /* HIP runtime error (Python: RuntimeError) */
@@ -141,6 +144,14 @@ int dppo_learn_f32(dppo_handle* h, const dppo_rollout* rollout, float* params, f
                    float* adam_v, const dppo_hparams* hp, const int32_t* host_perms,
                    const dppo_learn_outputs* outputs, void* stream);
 
+/* dppo_learn_f32 with the permutations given as their Fisher-Yates swap targets (host int32
+ * [E][T*N], dppo_perm_targets_numpy output): the shuffle itself is resolved on the device
+ * (dppo_perm_resolve), so the host only runs the MT19937 draws.  Same results bit for bit. */
+int dppo_learn_targets_f32(dppo_handle* h, const dppo_rollout* rollout, float* params,
+                           float* adam_m, float* adam_v, const dppo_hparams* hp,
+                           const int32_t* host_targets, const dppo_learn_outputs* outputs,
+                           void* stream);
+
 /* Gradient of the minibatch loss at `params` for samples idx[0..m) of the records built by
  * the last dppo_learn_f32/dppo_prepare_f32 (ppo.py:261-283), written to grad[P] (flat layout,
  * unclipped), plus, if loss4 is non-NULL, the loss terms to HOST loss4[4] = {loss, loss_policy,
@@ -162,17 +173,20 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
                        float max_norm, double lr, float beta1, float beta2, float eps, int64_t step,
                        float* out_norm, void* stream);
 
-/* The handle's pinned host staging buffer for the [E][T*N] permutations (waits for the previous
- * learn's upload of it to finish).  Generating permutations straight into it (dppo_perm_numpy)
- * and passing it to dppo_learn_f32 makes the upload a pure asynchronous DMA. */
-int dppo_perm_buffer(dppo_handle* h, int32_t** out);
+/* One of the handle's two pinned host staging buffers (slot 0 or 1) for the [E][T*N]
+ * permutations or swap targets; waits for the previous learn's upload from that slot to finish.
+ * Generating straight into a slot (dppo_perm_numpy / dppo_perm_targets_numpy) and passing it to
+ * dppo_learn_f32 / dppo_learn_targets_f32 makes the upload a pure asynchronous DMA; two slots let
+ * the next learn's draws run on the host while the current learn's upload is in flight. */
+int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every launch the
  * handle issues (off by default).  Classes, in order: old-policy eval, GAE, advantage-stat
- * reduce, record pack, fused minibatch gradient, slab reduce, clip+Adam, RCCL all-reduce.
+ * reduce, record pack, fused minibatch gradient, slab reduce, clip+Adam, RCCL all-reduce,
+ * Fisher-Yates resolution.
  * dppo_set_timing() synchronises the device and clears the records; dppo_get_timing()
  * synchronises and returns per-class summed milliseconds and launch counts. */
-#define DPPO_TIMING_CLASSES 8
+#define DPPO_TIMING_CLASSES 9
 int dppo_set_timing(dppo_handle* h, int32_t enable);
 int dppo_get_timing(dppo_handle* h, double* ms_sum, int64_t* counts);
 
@@ -185,11 +199,24 @@ int dppo_get_trace(dppo_handle* h, float* host_out, int32_t rows);
  * np.random.permutation would.  Host only. */
 int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
 
+/* The MT19937 half of dppo_perm_numpy: the Fisher-Yates swap targets out[c][i] = j_i
+ * (i = n-1 .. 1; out[c][0] = 0) of `count` successive permutations, advancing key/pos exactly
+ * as dppo_perm_numpy does.  Host only. */
+int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
+
+/* The swap half on the device: perms[c] = arange(n) shuffled by targets[c] (device int32
+ * [count][n]), identical to the sequential Fisher-Yates loop.  scratch: device int32
+ * [3 * count * n].  Stream-ordered. */
+int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
+                      int32_t* scratch, void* stream);
+
 /* Multi-GPU over RCCL (xGMI): rank 0 creates the id, the caller broadcasts it (e.g. with
  * torch.distributed), every rank attaches it to its handle.  dppo_learn_f32 then all-reduces the
  * advantage statistics once and the gradient once per minibatch. */
 int dppo_comm_unique_id(char* out128);
 int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128);
+
+#pragma GCC visibility pop
 
 #ifdef __cplusplus
 }

@@ -181,6 +181,11 @@ def test_learn_matches_reference_trace(name):
         np.testing.assert_allclose(outs["returns"].cpu().numpy() - outs["values"].cpu().numpy(),
                                    z["old/adv"][li].ravel(), atol=5e-5, err_msg="advantages")
         params_after.append(flat_params(agent))
+        # the global NumPy RNG ends where the reference left it (state before the next learn)
+        if li + 1 < n_learn:
+            st = np.random.get_state()
+            assert np.array_equal(st[1], z[f"rng_state_before{li + 1}"].astype(np.uint32))
+            assert st[2] == int(z[f"rng_pos_before{li + 1}"])
     np.testing.assert_allclose(losses, z["loss"], rtol=2e-5, atol=2e-5)
     np.testing.assert_allclose(norms, z["norm"], rtol=2e-5, atol=2e-5)
     names = list(z["param_names"])
@@ -191,9 +196,6 @@ def test_learn_matches_reference_trace(name):
         np.testing.assert_allclose(st["exp_avg"].cpu().numpy(), z[f"adam/{n}/exp_avg"],
                                    rtol=1e-3, atol=1e-7, err_msg=n)
         assert float(st["step"]) == float(z[f"adam/{names[0]}/step"])
-    # the global NumPy RNG ends where the reference left it
-    if n_learn == 1:
-        pass
     if bool(z["cfg/decay_lr"]):
         assert abs(agent.optimizer.param_groups[0]["lr"] - float(z[f"lr_after{n_learn - 1}"])) < 1e-12
 
@@ -298,3 +300,47 @@ def test_indivisible_minibatch_raises_value_error():
            for _ in range(3)]
     with pytest.raises(ValueError):
         agent.learn(exp)
+
+
+@pytest.mark.parametrize("n,count", [(1, 1), (2, 3), (3, 4), (17, 2), (1000, 4), (65539, 2),
+                                     (524288, 4)])
+def test_device_fisher_yates_resolution_matches_numpy(n, count):
+    """dppo_perm_resolve(host MT19937 targets) == np.random.permutation, bit-exact."""
+    np.random.seed(1000 + n)
+    key, pos, _ = N.mt_state()
+    tg = np.empty(count * n, np.int32)
+    N.perm_targets_numpy(key, pos, n, count, tg)
+    np.random.seed(1000 + n)
+    ref = np.concatenate([np.random.permutation(n) for _ in range(count)]).astype(np.int32)
+    td = t(tg, torch.int32)
+    out = torch.full((count * n,), -7, dtype=torch.int32, device=dev())
+    scratch = torch.empty(3 * count * n, dtype=torch.int32, device=dev())
+    N.perm_resolve(td.data_ptr(), out.data_ptr(), n, count, scratch.data_ptr(), stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_permutation_lookahead_hit_and_miss():
+    """The next learn's targets are drawn ahead on a host thread; they are used only while the
+    global NumPy RNG is untouched.  Interleaving foreign np.random draws must give exactly the
+    results of a learner without look-ahead, and leave the same RNG state."""
+    z = load_golden("learn_lunar_medium.npz")
+    results = []
+    for lookahead in (True, False):
+        agent = make_agent(z)
+        agent._learner.lookahead = lookahead
+        np.random.seed(11)
+        ro = diamond.engine.stage_experience(experience(z, 0), dev(), False)
+        agent.learn_device(ro)            # draws its own; the draft for learn 2 starts
+        agent.learn_device(ro)            # hit
+        np.random.random(3)               # foreign draw: the draft for learn 3 is now stale
+        agent.learn_device(ro)            # miss -> redrawn from the live state
+        agent.learn_device(ro)            # hit
+        torch.cuda.synchronize()
+        st = np.random.get_state()
+        results.append((flat_params(agent), st[1].copy(), st[2],
+                        agent._learner.host_seconds["lookahead_hits"]))
+    (p1, k1, q1, hits1), (p2, k2, q2, hits2) = results
+    assert np.array_equal(p1, p2)
+    assert np.array_equal(k1, k2) and q1 == q2
+    assert hits1 == 2 and hits2 == 0

@@ -74,6 +74,76 @@ def test_host_permutations_bit_exact_with_numpy(n):
     assert np.array_equal(after[1], ref_after[1]) and after[2] == ref_after[2]
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, (1 << 16) + 3])
+def test_host_swap_targets_replay_to_numpy_permutation(n):
+    """dppo_perm_targets_numpy = the MT19937 half of np.random.permutation: replaying its
+    targets with the sequential Fisher-Yates loop reproduces numpy, and the RNG ends in the same
+    state as after the full permutations."""
+    count = 3
+    np.random.seed(77 + n)
+    key, pos, st = N.mt_state()
+    tg = np.empty(count * n, np.int32)
+    pos = N.perm_targets_numpy(key, pos, n, count, tg)
+    np.random.seed(77 + n)
+    ref = [np.random.permutation(n) for _ in range(count)]
+    after = np.random.get_state()
+    assert np.array_equal(key, after[1]) and pos == after[2]
+    for c in range(count):
+        j = tg[c * n:(c + 1) * n]
+        assert j[0] == 0 and np.all(j <= np.arange(n)) and np.all(j >= 0)
+        assert np.array_equal(fisher_yates(j), ref[c])
+        assert np.array_equal(closed_form_shuffle(j), ref[c])
+
+
+def fisher_yates(j):
+    a = np.arange(len(j))
+    for i in range(len(j) - 1, 0, -1):
+        a[i], a[j[i]] = a[j[i]], a[i]
+    return a
+
+
+def closed_form_shuffle(j):
+    """NumPy restatement of the device resolution (csrc/shuffle.hip): with
+    succ(i) = min{i'' > i: j[i''] = j[i]}, M(q) = min{i'' > q: j[i''] = q}, W(q) = root of q under
+    M:  out[i] = W(succ(i)) if succ(i) exists else j[i];  out[0] = W(0)."""
+    n = len(j)
+    if n == 0:
+        return np.arange(0)
+    steps = np.arange(1, n)
+    # sort steps by (target, step): successor = next entry in the same target group
+    order = np.lexsort((steps, j[1:]))
+    s_sorted, t_sorted = steps[order], j[1:][order]
+    nxt_same = np.full(n - 1, -1)
+    same = t_sorted[1:] == t_sorted[:-1]
+    nxt_same[:-1][same] = s_sorted[1:][same]
+    succ = np.full(n, -1)
+    succ[s_sorted] = nxt_same
+    # M(q): smallest step > q targeting q
+    M = np.full(n, -1)
+    for q_steps_t, s in zip(t_sorted[::-1], s_sorted[::-1]):
+        if s > q_steps_t:
+            M[q_steps_t] = s
+    def root(q):
+        while M[q] >= 0:
+            q = M[q]
+        return q
+    out = np.empty(n, np.int64)
+    out[0] = root(0)
+    for i in range(1, n):
+        out[i] = root(succ[i]) if succ[i] >= 0 else j[i]
+    return out
+
+
+def test_closed_form_shuffle_on_adversarial_targets():
+    """All-zero, identity and random targets (every j_i <= i is a valid Fisher-Yates input)."""
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 5, 64, 300):
+        cases = [np.zeros(n, np.int64), np.arange(n), np.maximum(np.arange(n) - 1, 0),
+                 np.array([0] + [rng.integers(0, i + 1) for i in range(1, n)])]
+        for j in cases:
+            assert np.array_equal(closed_form_shuffle(j), fisher_yates(j))
+
+
 def test_host_permutations_match_golden_and_private_rng():
     d = load_golden("perm_seed42.npz")
     rs = np.random.RandomState(42)
