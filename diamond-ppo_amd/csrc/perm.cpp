@@ -17,6 +17,8 @@
 
 #include <cstdint>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "dppo_host.h"
 
@@ -123,6 +125,21 @@ void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
   g.pos = opos;
 }
 
+// a[0..n) holds Fisher-Yates targets on entry and the permutation on exit: the sequential
+// swap loop for i = n-1 .. 1, with the target lines prefetched ahead.
+void apply_swaps(int32_t* a, int64_t n) {
+  std::vector<int32_t> j(a, a + n);
+  for (int64_t k = 0; k < n; ++k) a[k] = (int32_t)k;
+  constexpr int kAhead = 16;
+  for (int64_t k = n - 1; k >= 1; --k) {
+    if (k - kAhead >= 1) __builtin_prefetch(a + j[k - kAhead], 1, 3);
+    const int32_t v = j[k];
+    const int32_t t = a[k];
+    a[k] = a[v];
+    a[v] = t;
+  }
+}
+
 bool bad_args(const uint32_t* key, const int32_t* pos, int64_t n, int32_t count,
               const int32_t* out) {
   return !key || !pos || !out || n < 0 || n > 0x7FFFFFFF || count < 0 || *pos < 0 || *pos > kN;
@@ -146,24 +163,20 @@ extern "C" int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t c
   if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
   MT g;
   g.load(key, *pos);
-  // targets first (into out itself), then the swaps in place with the target lines prefetched
-  // ahead -- the same state machine as numpy's fused loop
-  draw_targets(g, n, count, out);
-  int32_t* j = new int32_t[n > 1 ? n : 1];
+  // Targets first (into out itself), then the swaps in place -- the same state machine as
+  // numpy's fused loop.  The draws are one sequential MT19937 stream; the swaps of epoch c only
+  // need epoch c's targets, so at minibatch sizes each epoch's swaps run on a worker thread
+  // while the next epoch is drawn (wall ~ draws + one epoch's swaps).
+  const bool threaded = n >= (1 << 16) && count > 1;
+  std::vector<std::thread> workers;
   for (int32_t c = 0; c < count; ++c) {
-    int32_t* a = out + (int64_t)c * n;
-    std::memcpy(j, a, (size_t)n * sizeof(int32_t));
-    for (int64_t k = 0; k < n; ++k) a[k] = (int32_t)k;
-    constexpr int kAhead = 16;
-    for (int64_t k = n - 1; k >= 1; --k) {
-      if (k - kAhead >= 1) __builtin_prefetch(a + j[k - kAhead], 1, 3);
-      const int32_t v = j[k];
-      const int32_t t = a[k];
-      a[k] = a[v];
-      a[v] = t;
-    }
+    draw_targets(g, n, 1, out + (int64_t)c * n);
+    if (threaded)
+      workers.emplace_back(apply_swaps, out + (int64_t)c * n, n);
+    else
+      apply_swaps(out + (int64_t)c * n, n);
   }
-  delete[] j;
+  for (auto& w : workers) w.join();
   std::memcpy(key, g.mt, sizeof(g.mt));
   *pos = g.pos;
   return DPPO_OK;

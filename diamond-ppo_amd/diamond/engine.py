@@ -6,12 +6,14 @@ Adam buffers the gfx950 kernels update in place, keeps the reference's ``nn.Modu
 ``LinearLR`` behave exactly as in the reference), draws the minibatch permutations from the global
 NumPy RNG bit-exactly, and issues ONE native call per learn().
 
-Permutations (ppo.py:252-254) are split in two: the host runs NumPy's MT19937 draws (the
-Fisher-Yates swap targets, ``dppo_perm_targets_numpy``), the device resolves the swaps
-(``shuffle.hip``).  The draws for learn k+1 start on a host thread as soon as learn k is
-enqueued, from the RNG state learn k leaves behind; learn k+1 uses them only if the global NumPy
-RNG still holds exactly that state (otherwise it draws afresh), so the results and the RNG stream
-stay bit-identical to the reference's.
+Permutations (ppo.py:252-254) are produced off the critical path: the permutations for learn k+1
+are drawn on a host thread while learn k is enqueued and runs, from the RNG state learn k leaves
+behind (``dppo_perm_numpy``: one sequential MT19937 stream, each epoch's Fisher-Yates swaps on a
+worker thread of their own).  Learn k+1 uses them only if the global NumPy RNG still holds
+exactly that state (otherwise it draws afresh), so results and the RNG stream stay bit-identical
+to the reference's.  With ``DPPO_PERM_DEVICE=1`` the host only draws the swap targets and the GPU
+resolves the swaps (``shuffle.hip``, ``dppo_learn_targets_f32``) -- for hosts too slow to hide
+the swaps.
 
 Two paths, chosen once per agent:
 
@@ -220,6 +222,7 @@ class NativeLearner:
         self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "calls": 0,
                              "lookahead_hits": 0}
         self.lookahead = os.environ.get("DPPO_PERM_LOOKAHEAD", "1") != "0"
+        self.device_shuffle = os.environ.get("DPPO_PERM_DEVICE", "0") == "1"
         self._draft = None
         self._slot = 0
 
@@ -241,12 +244,14 @@ class NativeLearner:
         """Draw the next learn's swap targets on a host thread (ctypes releases the GIL)."""
         slot = 1 - self._slot
         buf = self.handle.perm_buffer(slot)
-        d = {"slot": slot, "buf": buf, "key_in": key.copy(), "pos_in": pos, "ok": False}
+        d = {"slot": slot, "buf": buf, "key_in": key.copy(), "pos_in": pos, "ok": False,
+             "device": self.device_shuffle}
+
+        draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
 
         def work():
             k = d["key_in"].copy()
-            d["pos_out"] = N.perm_targets_numpy(k, d["pos_in"], self.T * self.N,
-                                                self.cfg.num_epochs, buf)
+            d["pos_out"] = draw(k, d["pos_in"], self.T * self.N, self.cfg.num_epochs, buf)
             d["key_out"] = k
             d["ok"] = True
 
@@ -255,19 +260,22 @@ class NativeLearner:
         self._draft = d
 
     def _targets(self):
-        """This learn's swap targets in a pinned slot; advances the global NumPy RNG exactly as
-        num_epochs calls of np.random.permutation(B) would (ppo.py:254)."""
+        """This learn's permutations (or, with device_shuffle, their swap targets) in a pinned
+        slot; advances the global NumPy RNG exactly as num_epochs calls of
+        np.random.permutation(B) would (ppo.py:254)."""
         key, pos, st = N.mt_state()
         d, self._draft = self._draft, None
         if d is not None:
             d["thread"].join()
-            if d["ok"] and d["pos_in"] == pos and np.array_equal(d["key_in"], key):
+            if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos
+                    and np.array_equal(d["key_in"], key)):
                 self._slot = d["slot"]
                 N.set_mt_state(st, d["key_out"], d["pos_out"])
                 self.host_seconds["lookahead_hits"] += 1
                 return d["buf"], d["key_out"], d["pos_out"]
         buf = self.handle.perm_buffer(self._slot)
-        pos = N.perm_targets_numpy(key, pos, self.T * self.N, self.cfg.num_epochs, buf)
+        draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
+        pos = draw(key, pos, self.T * self.N, self.cfg.num_epochs, buf)
         N.set_mt_state(st, key, pos)
         return buf, key, pos
 
@@ -290,11 +298,12 @@ class NativeLearner:
                 self._start_draft(key, pos)
             t2 = time.perf_counter()
             hp = hparams(cfg, lr, step0)
-            N.check(self.handle.lib.dppo_learn_targets_f32(
-                self.handle.h, ctypes.byref(ro.as_struct()), self.flat.flat.data_ptr(),
-                self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
-                ctypes.byref(outputs) if outputs is not None else None, stream),
-                "dppo_learn_targets_f32")
+            fn = (self.handle.lib.dppo_learn_targets_f32 if self.device_shuffle
+                  else self.handle.lib.dppo_learn_f32)
+            N.check(fn(self.handle.h, ctypes.byref(ro.as_struct()), self.flat.flat.data_ptr(),
+                       self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
+                       ctypes.byref(outputs) if outputs is not None else None, stream),
+                    "dppo_learn_f32")
             t3 = time.perf_counter()
             hs = self.host_seconds
             hs["perms"] += t1 - t0

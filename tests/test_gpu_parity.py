@@ -148,14 +148,17 @@ def flat_params(agent):
     return np.concatenate([p.detach().cpu().numpy().ravel() for p in agent.network.parameters()])
 
 
-@pytest.mark.parametrize("name", LEARN_TRACES)
-def test_learn_matches_reference_trace(name):
+@pytest.mark.parametrize("name,device_shuffle",
+                         [(n, False) for n in LEARN_TRACES] + [("cartpole_decay", True),
+                                                               ("cheetah_small", True)])
+def test_learn_matches_reference_trace(name, device_shuffle):
     """Full drop-in learn() through the fused HIP path vs the reference's captured trace,
     including the NumPy-RNG minibatch order (global RNG set to the captured state)."""
     z = load_golden(f"learn_{name}.npz")
     T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
     agent = make_agent(z)
     assert agent._learner.fused
+    agent._learner.device_shuffle = device_shuffle
     E, M = int(z["cfg/num_epochs"]), int(z["cfg/num_minibatches"])
     losses, norms, params_after = [], [], []
     for li in range(n_learn):
@@ -320,15 +323,18 @@ def test_device_fisher_yates_resolution_matches_numpy(n, count):
     assert np.array_equal(out.cpu().numpy(), ref)
 
 
-def test_permutation_lookahead_hit_and_miss():
-    """The next learn's targets are drawn ahead on a host thread; they are used only while the
-    global NumPy RNG is untouched.  Interleaving foreign np.random draws must give exactly the
-    results of a learner without look-ahead, and leave the same RNG state."""
+@pytest.mark.parametrize("device_shuffle", [False, True])
+def test_permutation_lookahead_hit_and_miss(device_shuffle):
+    """The next learn's permutations are drawn ahead on a host thread; they are used only while
+    the global NumPy RNG is untouched.  Interleaving foreign np.random draws must give exactly the
+    results of a learner without look-ahead, and leave the same RNG state -- with the swaps on
+    the host or resolved on the device."""
     z = load_golden("learn_lunar_medium.npz")
     results = []
     for lookahead in (True, False):
         agent = make_agent(z)
         agent._learner.lookahead = lookahead
+        agent._learner.device_shuffle = device_shuffle
         np.random.seed(11)
         ro = diamond.engine.stage_experience(experience(z, 0), dev(), False)
         agent.learn_device(ro)            # draws its own; the draft for learn 2 starts
