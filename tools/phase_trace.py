@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Per-interval timing of the pipelined minibatch kernel (timing-only build).
+
+    make -C diamond-ppo_amd variant NAME=trace DEFS=-DDPPO_PHASE_TRACE
+    DPPO_LIB=diamond-ppo_amd/build/libdppo_trace.so python tools/phase_trace.py
+
+Runs one dppo_minibatch_grad_f32 launch on the CartPole bench shape and prints, for each of the
+NI barrier intervals of an interval set, the mean cycles each team spends issuing/draining its
+phase work (arrival - previous release) and the mean interval length (release - release),
+averaged over the steady-state sets of workgroup 0.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "diamond-ppo_amd"))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import diamond  # noqa: E402
+from diamond import _native as N  # noqa: E402
+
+NAMES0 = ["L1", "L2", "La/Lc", "heads+loss", "head bwd + gather"]
+NAMES1 = ["dZ2", "dZ1", "dW1+dWa", "dW2", "dWc"]
+NI = len(NAMES0)  # barriers per interval set
+
+
+def main():
+    T, Nn, D, A = 128, int(os.environ.get("ABL_N", "4096")), 4, 2
+    cfg = diamond.PPOConfig(rollout_steps=T, num_envs=Nn, verbose=False)
+    agent = diamond.PPO(None, cfg, envs=bench.SpecEnvs(D, A, False))
+    dev = agent.device
+    ro, _ = bench.synth_rollout(T, Nn, D, A, False, 0.02, 0.005, 0, dev)
+    agent.learn_device(ro)
+    torch.cuda.synchronize()
+    L = agent._learner
+    h = L.handle
+    hp = diamond.engine.hparams(cfg, cfg.lr, 0)
+    mb = T * Nn // 8
+    idx = torch.randperm(T * Nn, device=dev)[:mb].to(torch.int32)
+    g = torch.zeros(L.flat.total, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        N.check(h.lib.dppo_minibatch_grad_f32(h.h, L.flat.flat.data_ptr(), idx.data_ptr(), mb, mb,
+                                              ctypes.byref(hp), g.data_ptr(), None, s))
+    torch.cuda.synchronize()
+    buf = np.zeros((128, 8, 2), np.int64)
+    fn = h.lib.dppo_debug_phase_trace
+    fn.argtypes = [ctypes.c_void_p]
+    assert fn(buf.ctypes.data) == 0
+    arr, rel = buf[:, :, 0], buf[:, :, 1]
+    nbar = int((rel[:, 0] != 0).sum())
+    sets = nbar // NI
+    print(f"barriers traced: {nbar} ({sets} interval sets)")
+    work = np.zeros((nbar, 8))
+    span = np.zeros(nbar)
+    for k in range(1, nbar):
+        work[k] = arr[k] - rel[k - 1]
+        span[k] = rel[k].max() - rel[k - 1].max()
+    steady = [k for k in range(nbar) if 1 <= k // NI < sets - 1]
+    print(f"{'int':>3} {'team0 phase':>22} {'t0 cyc':>8} {'team1 phase':>10} {'t1 cyc':>8} "
+          f"{'interval':>9}")
+    tot = 0.0
+    for i in range(NI):
+        ks = [k for k in steady if k % NI == i]
+        w0 = work[ks][:, :4].max(axis=1).mean()
+        w1 = work[ks][:, 4:].max(axis=1).mean()
+        sp = span[ks].mean()
+        tot += sp
+        print(f"{i:>3} {NAMES0[i]:>22} {w0:8.0f} {NAMES1[i]:>10} {w1:8.0f} {sp:9.0f}")
+    print(f"set total {tot:.0f} cycles; whole launch {rel[nbar - 1].max() - rel[0].min():.0f} "
+          f"cycles from first to last barrier")
+
+
+if __name__ == "__main__":
+    main()
