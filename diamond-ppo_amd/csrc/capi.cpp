@@ -15,6 +15,7 @@
 namespace dppo {
 
 static thread_local char g_err[1024] = "";
+thread_local LaunchTiming g_launch_timing;
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -73,9 +74,18 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
-  int32_t* perms_dev = nullptr;     // [E][B] permutations the minibatch kernels gather with
-  int32_t* targets_dev = nullptr;   // [E][B] Fisher-Yates targets (dppo_learn_targets_f32)
+  // [E][B] permutations the minibatch kernels gather with, and the Fisher-Yates targets they are
+  // resolved from (dppo_learn_targets_f32); double-buffered so the next learn's upload can run
+  // on the copy stream while the current learn's minibatches still read the other buffer
+  int32_t* perms_dev2[2] = {nullptr, nullptr};
+  int32_t* targets_dev2[2] = {nullptr, nullptr};
+  int32_t* perms_dev = nullptr;     // the buffer of the learn being enqueued
   int32_t* perm_scratch = nullptr;  // [3][E][B] Fisher-Yates resolution scratch
+  int dev_slot = 0;
+  hipStream_t copy_stream = nullptr;  // H2D permutation uploads, overlapped with prepare()
+  hipEvent_t perms_ready = nullptr;   // upload of the current learn's permutations done
+  hipEvent_t perms_free[2] = {nullptr, nullptr};  // the last learn reading device slot k is done
+  bool perms_free_valid[2] = {false, false};
   // two pinned host staging slots, each with the event that marks its upload done
   int32_t* perms_pinned[2] = {nullptr, nullptr};
   hipEvent_t perm_copy_done[2] = {nullptr, nullptr};
@@ -194,26 +204,43 @@ hipEvent_t pool_event(dppo_handle* h) {
   return h->pool[h->pool_used++];
 }
 
-// RAII bracket: records a start/stop event pair around one launch when timing is enabled.
+// RAII bracket around the launches of one kernel class when timing is enabled.  Kernel brackets
+// hand their event pair to the launches (g_launch_timing, common.h), so the events carry the
+// kernels' own start/end times; `markers` brackets (RCCL calls) record the pair on the stream.
 struct Timed {
   dppo_handle* h;
   hipStream_t s;
   int cls;
-  hipEvent_t a = nullptr;
-  Timed(dppo_handle* h_, int cls_, hipStream_t s_) : h(h_), s(s_), cls(cls_) {
-    if (h->timing) {
-      a = pool_event(h);
-      if (a) (void)hipEventRecord(a, s);
+  bool markers;
+  hipEvent_t a = nullptr, b = nullptr;
+  Timed(dppo_handle* h_, int cls_, hipStream_t s_, bool markers_ = false)
+      : h(h_), s(s_), cls(cls_), markers(markers_) {
+    if (!h->timing) return;
+    a = pool_event(h);
+    b = pool_event(h);
+    if (!a || !b) {
+      a = b = nullptr;
+      return;
+    }
+    if (markers) {
+      (void)hipEventRecord(a, s);
+    } else {
+      g_launch_timing.start = a;
+      g_launch_timing.stop = b;
     }
   }
   ~Timed() {
-    if (h->timing && a) {
-      hipEvent_t b = pool_event(h);
-      if (b) {
+    if (!a) return;
+    if (markers) {
+      (void)hipEventRecord(b, s);
+    } else {
+      if (g_launch_timing.start == a) {  // nothing was launched: an empty interval
+        (void)hipEventRecord(a, s);
         (void)hipEventRecord(b, s);
-        h->recs.push_back({cls, a, b});
       }
+      g_launch_timing = LaunchTiming{};
     }
+    h->recs.push_back({cls, a, b});
   }
 };
 
@@ -261,7 +288,7 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
       DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, s));
     }
     if (h->comm && h->nranks > 1) {
-      Timed tm(h, K_COMM, s);
+      Timed tm(h, K_COMM, s, true);
       DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, s));
     }
   }
@@ -333,7 +360,7 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int3
                                 (d.continuous && h->rank == 0) ? 1 : 0, s));
   }
   if (h->comm && h->nranks > 1) {
-    Timed tm(h, K_COMM, s);
+    Timed tm(h, K_COMM, s, true);
     DPPO_TRY(allreduce(h, h->grad, (size_t)h->layout.total + 8, ncclFloat32, s));
   }
   return DPPO_OK;
@@ -343,18 +370,25 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int3
 
 namespace {
 
-// Upload the host [E][B] buffer (permutations or Fisher-Yates targets) to `dst`, stream-ordered.
-// A pinned slot is copied from directly (pure DMA); any other buffer is first staged in slot 0.
-int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, hipStream_t s) {
+// Upload the host [E][B] buffer (permutations or Fisher-Yates targets) into device buffer `dst`
+// (device slot `ds`) on the handle's copy stream, so the PCIe transfer (8 MB at B = 524,288) runs
+// beside the old-policy eval / GAE / pack kernels instead of in front of them.  The copy first
+// waits for the previous learn that read device slot `ds`; `perms_ready` marks the upload done
+// and the launch stream waits on it before the first kernel that reads the permutations.  A
+// pinned slot is copied from directly (pure DMA); any other buffer is first staged in slot 0.
+int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, int ds) {
   const size_t pbytes = (size_t)(h->dims.num_epochs * h->B) * sizeof(int32_t);
   int slot = host == h->perms_pinned[1] ? 1 : 0;
   if (host != h->perms_pinned[slot]) {
     if (h->perm_copy_pending[0]) DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done[0]));
     std::memcpy(h->perms_pinned[0], host, pbytes);
   }
-  DPPO_HIP_CHECK(
-      hipMemcpyAsync(dst, h->perms_pinned[slot], pbytes, hipMemcpyHostToDevice, s));
-  DPPO_HIP_CHECK(hipEventRecord(h->perm_copy_done[slot], s));
+  if (h->perms_free_valid[ds])
+    DPPO_HIP_CHECK(hipStreamWaitEvent(h->copy_stream, h->perms_free[ds], 0));
+  DPPO_HIP_CHECK(hipMemcpyAsync(dst, h->perms_pinned[slot], pbytes, hipMemcpyHostToDevice,
+                                h->copy_stream));
+  DPPO_HIP_CHECK(hipEventRecord(h->perm_copy_done[slot], h->copy_stream));
+  DPPO_HIP_CHECK(hipEventRecord(h->perms_ready, h->copy_stream));
   h->perm_copy_pending[slot] = true;
   return DPPO_OK;
 }
@@ -377,17 +411,19 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t s = S(stream);
   const int64_t E = d.num_epochs, M = d.num_minibatches;
-  // permutations (ppo.py:252-255): host -> pinned staging -> device, stream-ordered; given as
-  // swap targets they are shuffled on the device while nothing else depends on them yet
-  if (targets) {
-    DPPO_TRY(upload_perms(h, host_buf, h->targets_dev, s));
-    Timed tm(h, K_PERM, s);
-    DPPO_TRY(launch_perm_resolve(h->targets_dev, h->perms_dev, h->B, (int32_t)E, h->perm_scratch,
-                                 s));
-  } else {
-    DPPO_TRY(upload_perms(h, host_buf, h->perms_dev, s));
-  }
+  // permutations (ppo.py:252-255): host -> pinned staging -> device on the copy stream, beside
+  // prepare(); given as swap targets they are shuffled on the device after prepare()
+  const int ds = h->dev_slot;
+  h->dev_slot ^= 1;
+  h->perms_dev = h->perms_dev2[ds];
+  DPPO_TRY(upload_perms(h, host_buf, targets ? h->targets_dev2[ds] : h->perms_dev, ds));
   DPPO_TRY(prepare(h, rollout, params, hp, outputs, s));
+  DPPO_HIP_CHECK(hipStreamWaitEvent(s, h->perms_ready, 0));
+  if (targets) {
+    Timed tm(h, K_PERM, s);
+    DPPO_TRY(launch_perm_resolve(h->targets_dev2[ds], h->perms_dev, h->B, (int32_t)E,
+                                 h->perm_scratch, s));
+  }
   // (6) E x M dependent optimizer steps (ppo.py:258-285)
   const int32_t mb = h->mb;
   const int32_t m_total = mb * (h->comm ? h->nranks : 1);
@@ -415,6 +451,9 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
                                        inv_m, hp->value_loss_weight, hp->entropy_beta, s));
     }
   }
+  // device slot ds may be overwritten by an upload once this learn's minibatches are done
+  DPPO_HIP_CHECK(hipEventRecord(h->perms_free[ds], s));
+  h->perms_free_valid[ds] = true;
   h->last_stream = s;
   return DPPO_OK;
 }
@@ -492,9 +531,21 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
-  chk(dalloc(&h->perms_dev, E * h->B));
-  chk(dalloc(&h->targets_dev, E * h->B));
+  for (int k = 0; k < 2; ++k) {
+    chk(dalloc(&h->perms_dev2[k], E * h->B));
+    chk(dalloc(&h->targets_dev2[k], E * h->B));
+  }
+  h->perms_dev = h->perms_dev2[0];
   chk(dalloc(&h->perm_scratch, 3 * E * h->B));
+  if (rc == DPPO_OK) {
+    if (hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->perms_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->perms_free[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->perms_free[1], hipEventDisableTiming) != hipSuccess) {
+      set_error("hipStreamCreate / hipEventCreate failed");
+      rc = DPPO_EHIP;
+    }
+  }
   for (int k = 0; k < 2 && rc == DPPO_OK; ++k) {
     hipError_t e = hipHostMalloc((void**)&h->perms_pinned[k],
                                  (size_t)(E * h->B) * sizeof(int32_t), hipHostMallocDefault);
@@ -540,8 +591,13 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->partials);
   (void)hipFree(h->dsum);
   (void)hipFree(h->sq_part);
-  (void)hipFree(h->perms_dev);
-  (void)hipFree(h->targets_dev);
+  for (int k = 0; k < 2; ++k) {
+    (void)hipFree(h->perms_dev2[k]);
+    (void)hipFree(h->targets_dev2[k]);
+    if (h->perms_free[k]) (void)hipEventDestroy(h->perms_free[k]);
+  }
+  if (h->perms_ready) (void)hipEventDestroy(h->perms_ready);
+  if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   (void)hipFree(h->perm_scratch);
   for (int k = 0; k < 2; ++k) {
     if (h->perms_pinned[k]) (void)hipHostFree(h->perms_pinned[k]);
@@ -559,6 +615,7 @@ int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, cons
     return DPPO_EINVAL;
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
+  Timed tm(h, K_GAE, S(stream));
   return launch_gae(rewards, term, trunc, values, next_values, adv, returns, h->partials,
                     h->dims.rollout_steps, h->dims.num_envs, gamma, gae_lambda, S(stream),
                     &h->n_partials);
@@ -594,6 +651,7 @@ int dppo_old_policy_f32(dppo_handle* h, const float* params, const float* obs, c
   }
   DPPO_TRY(require_mlp(h));
   DPPO_HIP_CHECK(hipSetDevice(h->device));
+  Timed tm(h, K_EVAL, S(stream));
   return launch_eval(h->sh, h->po, params, obs, actions, next_obs, log_probs, values,
                      next_values, n, S(stream));
 }

@@ -1,6 +1,7 @@
 // Device-side common definitions for the gfx950 kernels of libdppo.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -28,6 +29,28 @@
   } while (0)
 
 namespace dppo {
+
+// Per-kernel timing (dppo_set_timing): while a timed bracket is open (capi.cpp), launches go
+// through hipExtLaunchKernel with the bracket's events, which the runtime stamps with the
+// kernel's own start and end -- no marker packets in the stream, so short kernels are timed as
+// rocprofv3 times them.  The first launch of a bracket takes the start event; every launch takes
+// the stop event (the last one's end wins).
+struct LaunchTiming {
+  hipEvent_t start = nullptr;
+  hipEvent_t stop = nullptr;
+};
+extern thread_local LaunchTiming g_launch_timing;
+
+#define DPPO_LAUNCH(K, G, B, SH, S, ...)                                          \
+  do {                                                                            \
+    ::dppo::LaunchTiming& lt_ = ::dppo::g_launch_timing;                          \
+    if (lt_.stop) {                                                               \
+      hipExtLaunchKernelGGL(K, G, B, SH, S, lt_.start, lt_.stop, 0, __VA_ARGS__); \
+      lt_.start = nullptr;                                                        \
+    } else {                                                                      \
+      hipLaunchKernelGGL(K, G, B, SH, S, __VA_ARGS__);                            \
+    }                                                                             \
+  } while (0)
 
 constexpr int kWave = 64;
 

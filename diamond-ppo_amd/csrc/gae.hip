@@ -7,14 +7,12 @@
 // Roofline: HBM-bound, 22 algorithmic bytes per element (rewards, values, next_values 4 B each,
 // term/trunc 1 B each read; advantages and returns 4 B each written), ~0.5 FLOP/B.
 //
-// Mapping: one workgroup (256 threads) owns a tile of kEnvTile envs x a chunk of T steps.  All
-// 256 threads stage the chunk's rows into LDS with 16-byte loads (each row is contiguous along
-// the env axis), then one lane per env runs the serial backward recurrence out of LDS in the
-// reference's exact fp32 operation order, and all threads write adv/returns back with 16-byte
-// stores.  The recurrence is serial per env (bit-exactness forbids re-association), but it is
-// only 2 dependent flops per step; the bytes are what cost, and they move with every lane of
-// the chip busy: N/kEnvTile workgroups (512 at N = 8192, several per CU so one tile's scan
-// overlaps the next tile's loads).
+// The recurrence is serial per env (bit-exactness forbids re-association) but only 2 dependent
+// flops per step; the bytes are what cost.  gae_pipe_kernel (below) overlaps the loads, the scan
+// and the stores of one env tile; gae_kernel is the plain stage-all / scan / store-all form, kept
+// for unaligned shapes (N not a multiple of 16 or unaligned buffers).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dppo {
@@ -140,6 +138,275 @@ __global__ __launch_bounds__(kThreads) void gae_kernel(
   }
 }
 
+// ---- Pipelined GAE (aligned shapes: the one learn() and the benchmark use) ---------------------
+// Persistent: at most one workgroup per CU, walking env tiles of E envs -- E = 32 (each row of a
+// [T][N] buffer one 128-B line) when that still gives every CU a tile, else E = 16 with blocks b
+// and b + 8 (one XCD under round-robin dispatch) taking the two halves of the same 128-B lines
+// (speed only).  The serial recurrence is the latency floor, so a workgroup scans ALL its envs in
+// one pass: lanes are free, the 128 dependent steps are not.  9 waves per workgroup:
+//  * waves 0..7 each own one 16-step chunk of the current 128-step super-chunk.  An owner loads
+//    its chunk (16-B loads along the env axis), computes every term of the recurrence that does
+//    not depend on the carried advantage -- delta = (r + (gamma*nv)*nt) - v and
+//    coef = (c*nt)*ntr, the reference's op order -- and writes them env-major into LDS, flags the
+//    chunk, waits until the scan has passed it, then stores advantages and returns = v + a
+//    (16-B stores) and accumulates the normalisation statistics;
+//  * wave 8 is the scan (lane = env): per chunk 8 ds_read_b128, then 16 dependent steps of
+//    a = delta + coef * a (two VALU ops each), 4 ds_write_b128.
+// An owner that has stored its chunk of tile i goes straight on to its chunk of tile i + 1, so
+// the chunks the scan reaches first (latest in time) start loading the next tile while the
+// scan is still walking back through the current one: loads and stores of different tiles
+// overlap.  Bit-exact with gae_step (same fp32 operations, FMA contraction off).
+constexpr int kPChunk = 16;
+constexpr int kPChunks = 8;
+constexpr int kPSuper = kPChunk * kPChunks;
+constexpr int kPThreads = (kPChunks + 1) * kWave;
+constexpr int kPStride = kPSuper + 4;
+
+#ifdef DPPO_GAE_TRACE
+// Timing-only build: workgroups 0 and 128 stamp s_memtime at the pipeline's hand-off points.
+// [wg][slot]: 0 start; 1+k owner k loads landed; 9+k owner k scan-wait done; 17+k owner k stores
+// issued; 25+k scanner chunk k flag seen; 33+k scanner chunk k done; 41 end.
+__device__ long long g_gae_trace[2][48];
+#define GAE_STAMP(slot)                                                                  \
+  do {                                                                                  \
+    if ((blockIdx.x == 0 || blockIdx.x == 128) && (threadIdx.x & 63) == 0 &&           \
+        (slot != 0 || threadIdx.x == 0) && (slot != 41 || threadIdx.x == 0))          \
+      g_gae_trace[blockIdx.x ? 1 : 0][slot] = __builtin_amdgcn_s_memtime();            \
+  } while (0)
+#else
+#define GAE_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif // env-major rows: 16-B aligned, conflict-free b128 reads
+
+template <int E>
+struct PipeLds {
+  float delta[E][kPStride];
+  float coef[E][kPStride];
+  float a[E][kPStride];
+  double wsum[kPChunks][2];
+  int loaded[kPChunks];
+  int scanned[kPChunks];
+  int issued[kPChunks];
+};
+
+__device__ __forceinline__ void gae_terms(float r, float v, float nv, float te, float tr, float g,
+                                          float c, float& delta, float& coef) {
+#pragma clang fp contract(off)
+  const float nt = 1.0f - te;                 // ppo.py:202-203
+  const float ntr = 1.0f - tr;
+  delta = (r + (g * nv) * nt) - v;            // ppo.py:206-210
+  coef = (c * nt) * ntr;                      // ppo.py:214-218
+}
+
+__device__ __forceinline__ float gae_carry(float delta, float coef, float a) {
+#pragma clang fp contract(off)
+  return delta + coef * a;                    // ppo.py:213-219
+}
+
+__device__ __forceinline__ void wait_flag(int* f, int gen) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
+    __builtin_amdgcn_s_sleep(1);
+}
+
+__device__ __forceinline__ void set_flag(int* f, int gen) {
+  __hip_atomic_store(f, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// logical tile lb -> env tile: lb and lb + 8 (same XCD under round-robin) get 2p and 2p + 1
+__device__ __forceinline__ int pipe_tile(int lb, int ntiles) {
+  const int grp = lb >> 4, r = lb & 15;
+  return (grp + 1) * 16 <= ntiles ? grp * 16 + 2 * (r & 7) + (r >> 3) : lb;
+}
+
+template <int E>
+__global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
+    const float* __restrict__ rew, const uint8_t* __restrict__ term,
+    const uint8_t* __restrict__ trunc, const float* __restrict__ val,
+    const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
+    double* __restrict__ partials, int T, int N, float g, float c, int ordered) {
+  __shared__ __attribute__((aligned(16))) PipeLds<E> L;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ntiles = N / E;
+  const int nsup = (T + kPSuper - 1) / kPSuper;
+  if (threadIdx.x < kPChunks) {
+    L.loaded[threadIdx.x] = 0;
+    L.scanned[threadIdx.x] = 0;
+    L.issued[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  GAE_STAMP(0);
+  if (wave < kPChunks) {
+    // ---------------- chunk owner
+    constexpr int V4 = E / 4;              // lanes per row (4 envs each)
+    constexpr int RP = kWave / V4;         // rows per pass
+    constexpr int PER = kPChunk / RP;      // passes per chunk (2 for E = 32, 1 for E = 16)
+    const int k = wave;
+    const int e0 = 4 * (lane % V4);
+    double lsum = 0.0, lsq = 0.0;
+    int gen = 0;
+    for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
+      const int n0 = (E == 16 ? pipe_tile(lb, ntiles) : lb) * E;
+      for (int s = 0; s < nsup; ++s) {
+        ++gen;
+        const int hi = T - s * kPSuper;
+        const int lo = hi > kPSuper ? hi - kPSuper : 0;
+        const int r0 = k * kPChunk;
+        const int nr = min(kPChunk, hi - lo - r0);
+        // chunks issue their loads latest-in-time first, the order the scan consumes them
+        if (ordered && k + 1 < kPChunks) wait_flag(&L.issued[k + 1], gen);
+        if (nr <= 0) {  // no such chunk in this super-chunk: the scan skips it too
+          if (lane == 0) __hip_atomic_store(&L.issued[k], gen, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+          continue;
+        }
+        f32x4 xr[PER], xv[PER], xn[PER];
+        uint32_t xt[PER], xu[PER];
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {  // every load of the chunk in flight at once
+          const int row = p * RP + lane / V4;
+          if (row < nr) {
+            const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
+            xr[p] = *(const f32x4*)(rew + go);
+            xv[p] = *(const f32x4*)(val + go);
+            xn[p] = *(const f32x4*)(nval + go);
+            xt[p] = *(const uint32_t*)(term + go);
+            xu[p] = *(const uint32_t*)(trunc + go);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == 0)
+          __hip_atomic_store(&L.issued[k], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+          const int row = p * RP + lane / V4;
+          if (row < nr) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float d, cf;
+              gae_terms(xr[p][j], xv[p][j], xn[p][j], ((xt[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f,
+                        ((xu[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f, g, c, d, cf);
+              L.delta[e0 + j][r0 + row] = d;
+              L.coef[e0 + j][r0 + row] = cf;
+            }
+          } else {
+            // rows past the end of the rollout: a = -0 + 1 * a is the identity for every a
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              L.delta[e0 + j][r0 + row] = -0.0f;
+              L.coef[e0 + j][r0 + row] = 1.0f;
+            }
+          }
+        }
+        if (lane == 0) set_flag(&L.loaded[k], gen);
+        GAE_STAMP(1 + k);
+        wait_flag(&L.scanned[k], gen);
+        GAE_STAMP(9 + k);
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+          const int row = p * RP + lane / V4;
+          if (row < nr) {
+            const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
+            f32x4 av;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
+            *(f32x4*)(adv + go) = av;
+            *(f32x4*)(ret + go) = xv[p] + av;  // returns = values + advantages (ppo.py:241)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              lsum += (double)av[j];
+              lsq += (double)av[j] * (double)av[j];
+            }
+          }
+        }
+        GAE_STAMP(17 + k);
+      }
+    }
+    // this wave's statistics partial (fixed shuffle tree)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      lsum += __shfl_xor(lsum, off);
+      lsq += __shfl_xor(lsq, off);
+    }
+    if (lane == 0) {
+      L.wsum[k][0] = lsum;
+      L.wsum[k][1] = lsq;
+    }
+  } else if (lane < E) {
+    // ---------------- the scan, one lane per env, always whole 16-row chunks (see the padding)
+    const int e = lane;
+    int gen = 0;
+    for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
+      float a = 0.0f;  // advantage carried backwards, 0 after the last step (ppo.py:198)
+      for (int s = 0; s < nsup; ++s) {
+        ++gen;
+        const int hi = T - s * kPSuper;
+        const int lo = hi > kPSuper ? hi - kPSuper : 0;
+        int k = (hi - lo + kPChunk - 1) / kPChunk - 1;
+        f32x4 d[4], cf[4];
+        wait_flag(&L.loaded[k], gen);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          d[q] = *(const f32x4*)&L.delta[e][k * kPChunk + 4 * q];
+          cf[q] = *(const f32x4*)&L.coef[e][k * kPChunk + 4 * q];
+        }
+        for (; k >= 0; --k) {
+          GAE_STAMP(25 + k);
+          // speculative prefetch of chunk k-1: its flag is read before its data (LDS operations of
+          // one wave complete in order), so a set flag proves the prefetched data is current
+          int pf = gen;
+          f32x4 nd[4], ncf[4];
+          if (k > 0) {
+            pf = __hip_atomic_load(&L.loaded[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              nd[q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
+              ncf[q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
+            }
+          }
+          f32x4 av[4];
+#pragma unroll
+          for (int j = kPChunk - 1; j >= 0; --j) {
+            a = gae_carry(d[j >> 2][j & 3], cf[j >> 2][j & 3], a);
+            av[j >> 2][j & 3] = a;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][k * kPChunk + 4 * q] = av[q];
+          if (lane == 0) set_flag(&L.scanned[k], gen);
+          GAE_STAMP(33 + k);
+          if (k > 0) {
+            if (pf < gen) {
+              wait_flag(&L.loaded[k - 1], gen);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                nd[q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
+                ncf[q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
+              }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              d[q] = nd[q];
+              cf[q] = ncf[q];
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  GAE_STAMP(41);
+  if (threadIdx.x == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int k = 0; k < kPChunks; ++k) {
+      s0 += L.wsum[k][0];
+      s1 += L.wsum[k][1];
+    }
+    partials[2 * blockIdx.x] = s0;
+    partials[2 * blockIdx.x + 1] = s1;
+  }
+}
+
 // Sum the per-tile partials in a fixed order: dsum = {sum, sumsq}.
 __global__ __launch_bounds__(256) void stats_reduce_kernel(const double* __restrict__ partials,
                                                            int n, double* __restrict__ dsum) {
@@ -241,6 +508,13 @@ inline int grid_for(int64_t n, int threads, int cap = 2048) {
 
 }  // namespace
 
+#ifdef DPPO_GAE_TRACE
+extern "C" __attribute__((visibility("default"))) int dppo_debug_gae_trace(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gae_trace), sizeof(g_gae_trace)) == hipSuccess ? 0
+                                                                                            : -2;
+}
+#endif
+
 int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
                const float* nv, float* adv, float* ret, double* partials, int T, int N,
                float gamma, float gae_lambda, hipStream_t s, int* n_partials) {
@@ -253,31 +527,60 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
                    ((uintptr_t)nv % 16 == 0) && ((uintptr_t)adv % 16 == 0) &&
                    ((uintptr_t)ret % 16 == 0) && ((uintptr_t)te % 16 == 0) &&
                    ((uintptr_t)tr % 16 == 0);
-  if (vec)
-    hipLaunchKernelGGL(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
+  // DPPO_GAE_STAGED=1 selects the earlier stage-all / scan / store-all kernel (A/B timing only)
+  static const bool staged = std::getenv("DPPO_GAE_STAGED") != nullptr;
+  // DPPO_GAE_UNORDERED=1: chunk owners issue their loads without the latest-first order (A/B)
+  static const int ordered = std::getenv("DPPO_GAE_UNORDERED") == nullptr ? 1 : 0;
+  if (vec && !staged) {
+    // persistent: at most one workgroup per CU, a multiple of 16 so XCD pairs stay aligned
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          cus <= 0)
+        cus = 256;
+    }
+    // DPPO_GAE_E / DPPO_GAE_WGS_PER_CU: tile width and residency overrides (A/B timing only)
+    static const int env_e = std::getenv("DPPO_GAE_E") ? std::atoi(std::getenv("DPPO_GAE_E")) : 0;
+    static const int per_cu =
+        std::getenv("DPPO_GAE_WGS_PER_CU") ? std::atoi(std::getenv("DPPO_GAE_WGS_PER_CU")) : 1;
+    const bool e32 = env_e == 32 ? N % 32 == 0 : (env_e == 16 ? false : (N % 32 == 0 && N / 32 >= cus));
+    const int tiles = e32 ? N / 32 : G;
+    int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
+    if (!e32 && grid >= 16) grid -= grid % 16;
+    *n_partials = grid;
+    if (e32)
+      DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
+                         adv, ret, partials, T, N, gamma, c, ordered);
+    else
+      DPPO_LAUNCH(gae_pipe_kernel<16>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
+                         adv, ret, partials, T, N, gamma, c, ordered);
+  } else if (vec)
+    DPPO_LAUNCH(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
                        partials, T, N, gamma, c);
   else
-    hipLaunchKernelGGL(gae_kernel<false>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv,
+    DPPO_LAUNCH(gae_kernel<false>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv,
                        ret, partials, T, N, gamma, c);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
 
 int launch_stats_reduce(const double* partials, int n_partials, double* dsum, hipStream_t s) {
-  hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, s, partials, n_partials, dsum);
+  DPPO_LAUNCH(stats_reduce_kernel, dim3(1), dim3(256), 0, s, partials, n_partials, dsum);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
 
 int launch_stats_finalize(const double* dsum, double n_total, float* mean_std, hipStream_t s) {
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(64), 0, s, dsum, n_total, mean_std);
+  DPPO_LAUNCH(stats_finalize_kernel, dim3(1), dim3(64), 0, s, dsum, n_total, mean_std);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
 
 int launch_adv_normalize(float* adv, const float* mean_std, int64_t n, hipStream_t s) {
   if (n <= 0) return DPPO_OK;
-  hipLaunchKernelGGL(adv_normalize_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, adv,
+  DPPO_LAUNCH(adv_normalize_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, adv,
                      mean_std, n);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
@@ -285,7 +588,7 @@ int launch_adv_normalize(float* adv, const float* mean_std, int64_t n, hipStream
 
 int launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.B <= 0) return DPPO_OK;
-  hipLaunchKernelGGL(pack_kernel, dim3(grid_for(a.B, 256)), dim3(256), 0, s, a);
+  DPPO_LAUNCH(pack_kernel, dim3(grid_for(a.B, 256)), dim3(256), 0, s, a);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

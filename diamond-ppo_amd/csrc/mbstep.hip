@@ -837,17 +837,17 @@ int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, in
   const dim3 grid((unsigned)G), block(kThreads);
   const bool c = sh.continuous != 0;
   if (sh.A <= 2) {
-    if (c) hipLaunchKernelGGL((mb_kernel<2, true>), grid, block, lds, s, k);
-    else hipLaunchKernelGGL((mb_kernel<2, false>), grid, block, lds, s, k);
+    if (c) DPPO_LAUNCH((mb_kernel<2, true>), grid, block, lds, s, k);
+    else DPPO_LAUNCH((mb_kernel<2, false>), grid, block, lds, s, k);
   } else if (sh.A <= 4) {
-    if (c) hipLaunchKernelGGL((mb_kernel<4, true>), grid, block, lds, s, k);
-    else hipLaunchKernelGGL((mb_kernel<4, false>), grid, block, lds, s, k);
+    if (c) DPPO_LAUNCH((mb_kernel<4, true>), grid, block, lds, s, k);
+    else DPPO_LAUNCH((mb_kernel<4, false>), grid, block, lds, s, k);
   } else if (sh.A <= 8) {
-    if (c) hipLaunchKernelGGL((mb_kernel<8, true>), grid, block, lds, s, k);
-    else hipLaunchKernelGGL((mb_kernel<8, false>), grid, block, lds, s, k);
+    if (c) DPPO_LAUNCH((mb_kernel<8, true>), grid, block, lds, s, k);
+    else DPPO_LAUNCH((mb_kernel<8, false>), grid, block, lds, s, k);
   } else {
-    if (c) hipLaunchKernelGGL((mb_kernel<16, true>), grid, block, lds, s, k);
-    else hipLaunchKernelGGL((mb_kernel<16, false>), grid, block, lds, s, k);
+    if (c) DPPO_LAUNCH((mb_kernel<16, true>), grid, block, lds, s, k);
+    else DPPO_LAUNCH((mb_kernel<16, false>), grid, block, lds, s, k);
   }
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;

@@ -777,17 +777,17 @@ KArgs base_args(const MlpShape& sh, const ParamOffsets& po, const float* params,
     const int A_ = (SH).A;                                                                   \
     const bool C_ = (SH).continuous != 0;                                                    \
     if (A_ <= 2) {                                                                           \
-      if (C_) hipLaunchKernelGGL((KERNEL<2, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
-      else hipLaunchKernelGGL((KERNEL<2, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);   \
+      if (C_) DPPO_LAUNCH((KERNEL<2, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
+      else DPPO_LAUNCH((KERNEL<2, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);   \
     } else if (A_ <= 4) {                                                                    \
-      if (C_) hipLaunchKernelGGL((KERNEL<4, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
-      else hipLaunchKernelGGL((KERNEL<4, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);   \
+      if (C_) DPPO_LAUNCH((KERNEL<4, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
+      else DPPO_LAUNCH((KERNEL<4, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);   \
     } else if (A_ <= 8) {                                                                    \
-      if (C_) hipLaunchKernelGGL((KERNEL<8, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
-      else hipLaunchKernelGGL((KERNEL<8, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);   \
+      if (C_) DPPO_LAUNCH((KERNEL<8, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
+      else DPPO_LAUNCH((KERNEL<8, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);   \
     } else {                                                                                 \
-      if (C_) hipLaunchKernelGGL((KERNEL<16, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
-      else hipLaunchKernelGGL((KERNEL<16, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);  \
+      if (C_) DPPO_LAUNCH((KERNEL<16, true>), GRID, dim3(kThreads), LDSB, STREAM, ARGS); \
+      else DPPO_LAUNCH((KERNEL<16, false>), GRID, dim3(kThreads), LDSB, STREAM, ARGS);  \
     }                                                                                        \
   } while (0)
 

@@ -133,7 +133,7 @@ int slab_reduce_blocks(int64_t p_total) { return (int)((p_total + 8 + kRedParams
 int launch_slab_reduce(const float* slabs, int G, int64_t slab_stride, int64_t p_total,
                        float* grad, double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
                        int add_entropy_const, hipStream_t s) {
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(slab_reduce_blocks(p_total)), dim3(256), 0, s,
+  DPPO_LAUNCH(slab_reduce_kernel, dim3(slab_reduce_blocks(p_total)), dim3(256), 0, s,
                      slabs, G, slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef,
                      add_entropy_const);
   DPPO_LAUNCH_CHECK();
@@ -147,7 +147,7 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
   int64_t g = (n + 255) / 256;
   if (g > 256) g = 256;
   if (g < 1) g = 1;
-  hipLaunchKernelGGL(clip_adam_kernel, dim3((unsigned)g), dim3(256), 0, s, params, grad, m, v, n,
+  DPPO_LAUNCH(clip_adam_kernel, dim3((unsigned)g), dim3(256), 0, s, params, grad, m, v, n,
                      sq_part, n_sq, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
                      out_norm, trace, inv_m, vf, ent);
   DPPO_LAUNCH_CHECK();

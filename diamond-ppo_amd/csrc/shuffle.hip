@@ -112,11 +112,11 @@ int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32
   int32_t* mq = scratch + 2 * total;
   DPPO_HIP_CHECK(hipMemsetAsync(head, 0xFF, (size_t)total * sizeof(int32_t), s));
   const int G = fy_grid(total);
-  fy_build_kernel<<<G, kBlock, 0, s>>>(targets, head, nxt, n, total);
+  DPPO_LAUNCH(fy_build_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, n, total);
   DPPO_LAUNCH_CHECK();
-  fy_links_kernel<<<G, kBlock, 0, s>>>(targets, head, nxt, mq, perms, n, total);
+  DPPO_LAUNCH(fy_links_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, mq, perms, n, total);
   DPPO_LAUNCH_CHECK();
-  fy_solve_kernel<<<G, kBlock, 0, s>>>(targets, mq, perms, n, total);
+  DPPO_LAUNCH(fy_solve_kernel, dim3(G), dim3(kBlock), 0, s, targets, mq, perms, n, total);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
