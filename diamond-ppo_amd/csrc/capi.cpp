@@ -74,6 +74,8 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
+  unsigned* arrivals = nullptr;  // reduce_adam_kernel's monotonic grid-arrival counter
+  unsigned radam_epoch = 0;      // reduce_adam launches so far on this handle
   // [E][B] permutations the minibatch kernels gather with, and the Fisher-Yates targets they are
   // resolved from (dppo_learn_targets_f32); double-buffered so the next learn's upload can run
   // on the copy stream while the current learn's minibatches still read the other buffer
@@ -192,7 +194,7 @@ int dalloc(T** p, int64_t n) {
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
 enum KClass {
-  K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_PERM, K_NCLASS
+  K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_PERM, K_RADAM, K_NCLASS
 };
 
 hipEvent_t pool_event(dppo_handle* h) {
@@ -432,23 +434,51 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
     for (int64_t j = 0; j < M; ++j) {
       const int64_t k = e * M + j;
       const int32_t* idx = h->perms_dev + e * h->B + j * mb;
-      DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
       const double step = (double)(hp->adam_step + k + 1);
       const double bc1 = 1.0 - std::pow((double)hp->adam_beta1, step);
       const double bc2 = 1.0 - std::pow((double)hp->adam_beta2, step);
       const double step_size = hp->lr / bc1;
       const double bc2_sqrt = std::pow(bc2, 0.5);
-      Timed tm(h, K_ADAM, s);
-      // single device: the norm comes from the reduce kernel's per-block partials; after an
-      // all-reduce those are stale, so the Adam kernel recomputes it from the gradient
+      float* trace = h->trace + k * DPPO_TRACE_FIELDS;
       const bool multi = h->comm && h->nranks > 1;
-      DPPO_TRY(launch_clip_adam_traced(params, h->grad, adam_m, adam_v, h->layout.total,
-                                       multi ? nullptr : h->sq_part,
+      if (!multi) {
+        // single device: fused kernel -> slab reduce + clip + Adam in one launch
+        GradArgs ga{};
+        ga.params = params;
+        ga.rec = h->rec;
+        ga.idx = idx;
+        ga.m = mb;
+        ga.inv_m = inv_m;
+        ga.clip_eps = hp->ppo_clip;
+        ga.vf_coef = hp->value_loss_weight;
+        ga.ent_coef = hp->entropy_beta;
+        ga.slabs = h->slabs;
+        ga.slab_stride = h->slab_stride;
+        ga.p_total = h->layout.total;
+        int G = mb_grid(mb);
+        if (G > h->G) G = h->G;
+        {
+          Timed tm(h, K_GRAD, s);
+          DPPO_TRY(launch_mb(h->sh, h->po, ga, G, s));
+        }
+        Timed tm(h, K_RADAM, s);
+        DPPO_TRY(launch_reduce_adam(
+            h->slabs, G, h->slab_stride, h->layout.total, h->grad, h->sq_part, h->po.ls,
+            d.continuous ? d.act_dim : 0, hp->entropy_beta, d.continuous ? 1 : 0, h->arrivals,
+            ++h->radam_epoch, params, adam_m, adam_v, hp->grad_norm_clip, (float)(-step_size), (float)bc2_sqrt,
+            hp->adam_beta1, hp->adam_beta2, hp->adam_eps, trace, inv_m, hp->value_loss_weight,
+            hp->entropy_beta, s));
+        continue;
+      }
+      DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
+      Timed tm(h, K_ADAM, s);
+      // after the all-reduce the reduce kernel's per-block norm partials are stale: the Adam
+      // kernel recomputes the norm from the gradient itself
+      DPPO_TRY(launch_clip_adam_traced(params, h->grad, adam_m, adam_v, h->layout.total, nullptr,
                                        slab_reduce_blocks(h->layout.total), hp->grad_norm_clip,
-                                       (float)(-step_size),
-                                       (float)bc2_sqrt, hp->adam_beta1, hp->adam_beta2,
-                                       hp->adam_eps, nullptr, h->trace + k * DPPO_TRACE_FIELDS,
-                                       inv_m, hp->value_loss_weight, hp->entropy_beta, s));
+                                       (float)(-step_size), (float)bc2_sqrt, hp->adam_beta1,
+                                       hp->adam_beta2, hp->adam_eps, nullptr, trace, inv_m,
+                                       hp->value_loss_weight, hp->entropy_beta, s));
     }
   }
   // device slot ds may be overwritten by an upload once this learn's minibatches are done
@@ -531,6 +561,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
+  chk(dalloc(&h->arrivals, 16));
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->B));
     chk(dalloc(&h->targets_dev2[k], E * h->B));
@@ -561,6 +592,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   if (rc == DPPO_OK) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
+    (void)hipMemset(h->arrivals, 0, 16 * sizeof(unsigned));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }
@@ -591,6 +623,7 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->partials);
   (void)hipFree(h->dsum);
   (void)hipFree(h->sq_part);
+  (void)hipFree(h->arrivals);
   for (int k = 0; k < 2; ++k) {
     (void)hipFree(h->perms_dev2[k]);
     (void)hipFree(h->targets_dev2[k]);

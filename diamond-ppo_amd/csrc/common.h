@@ -85,7 +85,6 @@ int launch_pack(const PackArgs& a, hipStream_t s);
 struct MlpShape {
   int D, D8, A, continuous, R;  // R = record stride (floats)
 };
-size_t mlp_lds_bytes_grad(const MlpShape& sh);
 size_t mlp_lds_bytes_eval(const MlpShape& sh);
 int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                 const void* actions, const float* next_obs, float* logp, float* values,
@@ -101,14 +100,11 @@ struct GradArgs {
   int64_t slab_stride; // floats per slab (param total + 8 loss slots, rounded)
   int64_t p_total;
 };
-int grad_grid(int32_t m);
 // Feature-split fused minibatch kernel (mbstep.hip), the one learn() uses.
 size_t mb_lds_bytes(const MlpShape& sh);
 int mb_grid(int32_t m);
 int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
               hipStream_t s);
-int launch_grad(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
-                hipStream_t s);
 
 // Optimiser kernels: optim.hip.
 int slab_reduce_blocks(int64_t p_total);
@@ -119,6 +115,14 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
                             const double* sq_part, int n_sq, float max_norm, float neg_step_size,
                             float bc2_sqrt, float beta1, float beta2, float eps, float* out_norm,
                             float* trace, float inv_m, float vf, float ent, hipStream_t s);
+// slab reduce + clip + Adam fused (single device): `arrivals` = a device counter zeroed once;
+// launch number `epoch` (1, 2, ...) on it waits for epoch x blocks arrivals
+int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p_total, float* grad,
+                       double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
+                       int add_entropy_const, unsigned* arrivals, unsigned epoch, float* params,
+                       float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
+                       float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
+                       float ent, hipStream_t s);
 int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, float max_norm,
                      float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
                      float* out_norm, hipStream_t s);

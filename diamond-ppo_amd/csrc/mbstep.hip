@@ -189,6 +189,19 @@ __device__ __forceinline__ void mm_rows(f32x4 (&acc)[NSB], const float (&w)[NT],
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// mm_rows for a first layer of K = 4 * NT <= 16 inputs (one 16-column block): NT MFMAs per tile.
+template <int NT>
+__device__ __forceinline__ void mm_rows_lo(f32x4 (&acc)[NSB], const float (&w)[8], const float* X,
+                                           int stride, int l15, int h4) {
+  f32x4 b[NSB];
+#pragma unroll
+  for (int sb = 0; sb < NSB; ++sb) b[sb] = *(const f32x4*)(X + (16 * sb + l15) * stride + 4 * h4);
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb) acc[sb] = mfma16(w[j], b[sb][j], acc[sb]);
+}
+
 // Write a wave's output rows (16q + 4h4 + r, sample 16sb + l15) into an image (permuted cols).
 __device__ __forceinline__ void put_rows(float* X, int stride, int col0, const f32x4 (&v)[NSB],
                                          int l15, int h4) {
@@ -398,12 +411,12 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       if (act) {
         f32x4 h1r[NSB];
         init_bias(h1r, lds + L.b1, row0, h4);
-        if (nk1 == 8) {
-          mm_rows<8>(h1r, w1f, X0, SX0, l15, h4);
-        } else {
-          const float w1h[4] = {w1f[0], w1f[1], w1f[2], w1f[3]};
-          mm_rows<4>(h1r, w1h, X0, SX0, l15, h4);
-        }
+        // k-steps t cover inputs 4t .. 4t+3: only ceil(D/4) of them are non-zero
+        if (a.D > 16) mm_rows<8>(h1r, w1f, X0, SX0, l15, h4);
+        else if (a.D > 12) mm_rows_lo<4>(h1r, w1f, X0, SX0, l15, h4);
+        else if (a.D > 8) mm_rows_lo<3>(h1r, w1f, X0, SX0, l15, h4);
+        else if (a.D > 4) mm_rows_lo<2>(h1r, w1f, X0, SX0, l15, h4);
+        else mm_rows_lo<1>(h1r, w1f, X0, SX0, l15, h4);
         tanh_rows(h1r);
         put_rows(H1, SA, row0, h1r, l15, h4);
       }
@@ -679,6 +692,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       if (i < 2) gW1[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
     f32x4 gb1 = (f32x4){0.f, 0.f, 0.f, 0.f}, gb2 = gb1;  // hidden-bias partials (b1, b2 rows)
+    // (a static s_setprio 1 for this younger, MFMA-heavy half measured 3-4 % slower: the forward
+    // team's VALU phases are the critical path)
     __syncthreads();  // LDS head weights / biases visible (pairs with team 0's)
 #ifdef DPPO_PHASE_TRACE
     int tr_k_ = 0;
@@ -725,15 +740,18 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         put_rows(DZ1, SA, row0, dz1, l15, h4);
       }
       STEP_BARRIER();
-      // ---- (3) dW1 += dZ1 X0^T ; dWa += dZa H2^T  (team 0 runs its MFMA-heavy layer here)
+      // ---- (3) dW1 += dZ1 X0^T only: team 0 runs its MFMA-heavy actor / critic layers here
+      // (dW1 cannot move later: team 0 gathers the next step into this X0 buffer in interval 5)
       if (act) {
         if (nk1 == 8) wgrad16<2>(gW1, DZ1, SA, 0, X0, SX0, 0, row0, l15, h4);
         else wgrad16<1>(gW1, DZ1, SA, 0, X0, SX0, 0, row0, l15, h4);
-        wgrad16<4>(gWa, DZAC, SAC, 0, H2, SA, 0, row0, l15, h4);
       }
       STEP_BARRIER();
-      // ---- (4) dW2 += dZ2 H1^T  (team 0: heads + loss on VALU)
-      if (act) wgrad16<4>(gW2, DZ2, SA, 0, H1, SA, 0, row0, l15, h4);
+      // ---- (4) dWa += dZa H2^T ; dW2 += dZ2 H1^T  (team 0: heads + loss on VALU)
+      if (act) {
+        wgrad16<4>(gWa, DZAC, SAC, 0, H2, SA, 0, row0, l15, h4);
+        wgrad16<4>(gW2, DZ2, SA, 0, H1, SA, 0, row0, l15, h4);
+      }
       STEP_BARRIER();
       // ---- (5) dWc += dZc H2^T  (team 0: head back-propagation on VALU)
       if (act) wgrad16<4>(gWc, DZAC, SAC, 64, H2, SA, 0, row0, l15, h4);

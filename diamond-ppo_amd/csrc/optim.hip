@@ -69,6 +69,56 @@ __device__ __forceinline__ double block_sum(double v, double* sh) {
   return t;
 }
 
+// One Adam element in torch _single_tensor_adam's op order (no FMA contraction).
+__device__ __forceinline__ void adam_elem(float* __restrict__ params, const float* __restrict__ grad,
+                                          float* __restrict__ m, float* __restrict__ v,
+                                          int64_t k, float coef, float w1, float w2, float beta2,
+                                          float bc2_sqrt, float eps, float neg_step_size) {
+#pragma clang fp contract(off)
+  const float g = grad[k] * coef;
+  float mk = m[k];
+  mk = mk + w1 * (g - mk);                 // lerp, weight < 0.5 branch
+  float vk = v[k] * beta2;
+  vk = vk + (w2 * g) * g;                  // addcmul_(g, g, value = 1 - beta2)
+  const float denom = sqrtf(vk) / bc2_sqrt + eps;
+  params[k] = params[k] + neg_step_size * (mk / denom);
+  m[k] = mk;
+  v[k] = vk;
+}
+
+// adam_elem on registers (same operations, same order)
+__device__ __forceinline__ void adam_regs(float& p, float gr, float& mk, float& vk, float coef,
+                                          float w1, float w2, float beta2, float bc2_sqrt,
+                                          float eps, float neg_step_size) {
+#pragma clang fp contract(off)
+  const float g = gr * coef;
+  mk = mk + w1 * (g - mk);
+  vk = vk * beta2;
+  vk = vk + (w2 * g) * g;
+  const float denom = sqrtf(vk) / bc2_sqrt + eps;
+  p = p + neg_step_size * (mk / denom);
+}
+
+__device__ __forceinline__ float clip_coef(double sumsq, float max_norm, float* norm_out) {
+  const float norm = (float)sqrt(sumsq);
+  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1, always applied (clip_grad.py:165-169)
+  float coef = max_norm / (norm + 1e-6f);
+  *norm_out = norm;
+  return coef < 1.0f ? coef : 1.0f;
+}
+
+__device__ __forceinline__ void write_trace(float* trace, const float* grad, int64_t n, float norm,
+                                            float inv_m, float vf, float ent) {
+  const float lpi = grad[n + 0] * inv_m;
+  const float lv = grad[n + 1] * inv_m;
+  const float h = grad[n + 2] * inv_m;
+  trace[0] = lpi + vf * lv - ent * h;  // ppo.py:276-280
+  trace[1] = lpi;
+  trace[2] = lv;
+  trace[3] = h;
+  trace[4] = norm;
+}
+
 // grad: [n] flat gradient followed by 8 loss slots {sum l_pi, sum l_v, sum H, ...}.
 // sq_part/n_sq: per-block partial sums of squares of grad (null => recompute from grad).
 __global__ __launch_bounds__(256) void clip_adam_kernel(
@@ -93,37 +143,102 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
     for (; k < n; k += 256) sq += (double)grad[k] * (double)grad[k];
   }
   const double tot = block_sum(sq, sh);
-  const float norm = (float)sqrt(tot);
-  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1, always applied (clip_grad.py:165-169)
-  float coef = max_norm / (norm + 1e-6f);
-  coef = coef < 1.0f ? coef : 1.0f;
+  float norm;
+  const float coef = clip_coef(tot, max_norm, &norm);
   const float w1 = 1.0f - beta1;
   const float w2 = 1.0f - beta2;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const float g = grad[k] * coef;
-    float mk = m[k];
-    mk = mk + w1 * (g - mk);                 // lerp, weight < 0.5 branch
-    float vk = v[k] * beta2;
-    vk = vk + (w2 * g) * g;                  // addcmul_(g, g, value = 1 - beta2)
-    const float denom = sqrtf(vk) / bc2_sqrt + eps;
-    params[k] = params[k] + neg_step_size * (mk / denom);
-    m[k] = mk;
-    v[k] = vk;
-  }
+       k += (int64_t)gridDim.x * blockDim.x)
+    adam_elem(params, grad, m, v, k, coef, w1, w2, beta2, bc2_sqrt, eps, neg_step_size);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (out_norm) *out_norm = norm;
-    if (trace) {
-      const float lpi = grad[n + 0] * inv_m;
-      const float lv = grad[n + 1] * inv_m;
-      const float h = grad[n + 2] * inv_m;
-      trace[0] = lpi + vf * lv - ent * h;  // ppo.py:276-280
-      trace[1] = lpi;
-      trace[2] = lv;
-      trace[3] = h;
-      trace[4] = norm;
-    }
+    if (trace) write_trace(trace, grad, n, norm, inv_m, vf, ent);
   }
+}
+
+// Slab reduction + clip_grad_norm_ + Adam in ONE launch (single device).  Every block reduces its
+// 64 parameters as slab_reduce_kernel does and publishes them and its sum of squares
+// write-through (sc1 stores, the storing wave drained); then all blocks meet in a grid-wide
+// arrival count (a monotonic counter: launch `epoch` waits for epoch x gridDim arrivals, so it is
+// never reset), each acquires (agent scope), sums the per-block squares in a fixed order and
+// applies Adam to its own 64 parameters, whose gradients it still holds in registers and whose
+// moments it prefetched before the wait.  The grid (~210 blocks of 256 threads) is always
+// resident; the wait is bounded.  (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
+// price list: fanin vs boundary.)
+__global__ __launch_bounds__(256) void reduce_adam_kernel(
+    const float* __restrict__ slabs, int G, int64_t stride, int64_t p_total, float* grad,
+    double* sq_part, int64_t ls_off, int ls_n, float ent_coef, int add_entropy_const,
+    unsigned* arrivals, unsigned epoch, float* __restrict__ params, float* __restrict__ m,
+    float* __restrict__ v, float max_norm, float neg_step_size, float bc2_sqrt, float beta1,
+    float beta2, float eps, float* __restrict__ trace, float inv_m, float vf, float ent) {
+#pragma clang fp contract(off)
+  __shared__ float part[4][kRedParams];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
+  const int64_t n = p_total + 8;
+  float s = 0.0f;
+  if (p < n) {
+    const float* src = slabs + p;
+    int g = wave;
+    for (; g + 60 < G; g += 64) {
+      float x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = src[(int64_t)(g + 4 * k) * stride];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += x[k];
+    }
+    for (; g < G; g += 4) s += src[(int64_t)g * stride];
+  }
+  part[wave][lane] = s;
+  // this block's Adam operands, loaded while the other blocks finish
+  float mk = 0.f, vk = 0.f, pk = 0.f;
+  if (wave == 0 && p < p_total) {
+    mk = m[p];
+    vk = v[p];
+    pk = params[p];
+  }
+  __syncthreads();
+  float t = 0.f;
+  if (wave == 0) {
+    t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
+    if (p < n) __hip_atomic_store(grad + p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    double q = (p < p_total) ? (double)t * (double)t : 0.0;
+    for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+    if (lane == 0)
+      __hip_atomic_store(sq_part + blockIdx.x, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains (R1)
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = epoch * gridDim.x;
+    for (int spins = 0; (int)(__hip_atomic_load(arrivals, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
+         ++spins) {
+      if (spins > (1 << 22)) break;  // never expected: the grid is resident
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // global norm: every block sums the same per-block squares in the same order
+  double sq = 0.0;
+  for (int k = lane; k < (int)gridDim.x; k += 64) sq += sq_part[k];
+  for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+  float norm;
+  const float coef = clip_coef(sq, max_norm, &norm);
+  if (p < p_total) {
+    adam_regs(pk, t, mk, vk, coef, 1.0f - beta1, 1.0f - beta2, beta2, bc2_sqrt, eps,
+              neg_step_size);
+    params[p] = pk;
+    m[p] = mk;
+    v[p] = vk;
+  }
+  // the loss slots (published by the block past the last parameter) for the trace
+  if (blockIdx.x == 0 && lane == 0 && trace) write_trace(trace, grad, p_total, norm, inv_m, vf, ent);
 }
 
 }  // namespace
@@ -150,6 +265,20 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
   DPPO_LAUNCH(clip_adam_kernel, dim3((unsigned)g), dim3(256), 0, s, params, grad, m, v, n,
                      sq_part, n_sq, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
                      out_norm, trace, inv_m, vf, ent);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p_total, float* grad,
+                       double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
+                       int add_entropy_const, unsigned* arrivals, unsigned epoch, float* params,
+                       float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
+                       float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
+                       float ent, hipStream_t s) {
+  DPPO_LAUNCH(reduce_adam_kernel, dim3(slab_reduce_blocks(p_total)), dim3(256), 0, s, slabs, G,
+              slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef, add_entropy_const,
+              arrivals, epoch, params, m, v, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
+              trace, inv_m, vf, ent);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

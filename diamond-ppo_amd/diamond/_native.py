@@ -31,7 +31,7 @@ EXPORTED = [
     "dppo_perm_targets_numpy", "dppo_perm_resolve",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
-                  "allreduce", "perm"]
+                  "allreduce", "perm", "reduce_adam"]
 
 
 class Dims(ctypes.Structure):

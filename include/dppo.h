@@ -180,13 +180,14 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
  * the next learn's draws run on the host while the current learn's upload is in flight. */
 int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out);
 
-/* Per-kernel timing with HIP events recorded on the launch stream around every launch the
- * handle issues (off by default).  Classes, in order: old-policy eval, GAE, advantage-stat
- * reduce, record pack, fused minibatch gradient, slab reduce, clip+Adam, RCCL all-reduce,
- * Fisher-Yates resolution.
+/* Per-kernel timing with HIP events (off by default): while enabled, every kernel the handle
+ * launches carries a start/stop event pair stamped with the kernel's own execution interval
+ * (hipExtLaunchKernel), RCCL calls a pair of stream markers.  Classes, in order: old-policy eval,
+ * GAE, advantage-stat reduce, record pack, fused minibatch gradient, slab reduce, clip+Adam, RCCL
+ * all-reduce, Fisher-Yates resolution, fused slab reduce + clip + Adam (single device).
  * dppo_set_timing() synchronises the device and clears the records; dppo_get_timing()
  * synchronises and returns per-class summed milliseconds and launch counts. */
-#define DPPO_TIMING_CLASSES 9
+#define DPPO_TIMING_CLASSES 10
 int dppo_set_timing(dppo_handle* h, int32_t enable);
 int dppo_get_timing(dppo_handle* h, double* ms_sum, int64_t* counts);
 

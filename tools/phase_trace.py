@@ -25,7 +25,7 @@ import diamond  # noqa: E402
 from diamond import _native as N  # noqa: E402
 
 NAMES0 = ["L1", "L2", "La/Lc", "heads+loss", "head bwd + gather"]
-NAMES1 = ["dZ2", "dZ1", "dW1+dWa", "dW2", "dWc"]
+NAMES1 = ["dZ2", "dZ1", "dW1", "dWa+dW2", "dWc"]
 NI = len(NAMES0)  # barriers per interval set
 
 
