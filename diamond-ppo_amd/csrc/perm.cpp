@@ -15,6 +15,8 @@
 // dppo_perm_targets_numpy stops after the draws: the swaps are resolved on the GPU instead
 // (shuffle.hip), which takes the sequential swap chain off the host's critical path.
 
+#include <immintrin.h>
+
 #include <cstdint>
 #include <cstring>
 #include <thread>
@@ -33,7 +35,7 @@ constexpr uint32_t kLower = 0x7FFFFFFFu;
 // One MT19937 block: twist the 624-word state and temper it into out[].  The three twist
 // ranges only depend on words at distance >= 227 (or the block before), so each loop
 // vectorises; AVX2 clones are picked at load time where the host has them.
-__attribute__((target_clones("avx2", "default"))) void twist_block(uint32_t* __restrict mt,
+__attribute__((target_clones("avx512f", "avx2", "default"))) void twist_block(uint32_t* __restrict mt,
                                                                    uint32_t* __restrict out) {
   int i = 0;
   for (; i < kN - kM; ++i) {
@@ -85,6 +87,43 @@ inline uint32_t smear(uint32_t m) {
   return m;
 }
 
+// AVX-512 draws, 16 per step.  Inside a mask band a draw is accepted iff v <= i, and i falls by
+// at most one per draw, so over a group of 16 draws starting at i every v <= i - 15 is accepted
+// and every v > i rejected whatever the others do: the group's outcome needs no serial chain
+// unless some v lands in (i - 15, i].  The accepted draws, in order, are the targets j[i],
+// j[i-1], ...: one compress, one reversal, one masked store.  Returns the words consumed; stops
+// at the first ambiguous group, when i < lo + 15 (the band's last draws) or at the block end.
+__attribute__((target("avx512f,avx512vl"))) uint32_t draw_groups_avx512(const uint32_t* o,
+                                                                         uint32_t words,
+                                                                         uint32_t mask, uint32_t& i,
+                                                                         uint32_t lo, int32_t* j) {
+  const __m512i vmask = _mm512_set1_epi32((int)mask);
+  const __m512i rev = _mm512_set_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  uint32_t k = 0;
+  uint32_t ii = i;
+  while (k + 16 <= words && ii >= lo + 15) {
+    const __m512i v = _mm512_and_si512(_mm512_loadu_si512((const void*)(o + k)), vmask);
+    const __mmask16 acc = _mm512_cmple_epu32_mask(v, _mm512_set1_epi32((int)(ii - 15)));
+    const __mmask16 amb =
+        (__mmask16)(_mm512_cmple_epu32_mask(v, _mm512_set1_epi32((int)ii)) & ~acc);
+    if (amb) break;
+    const int cnt = __builtin_popcount((unsigned)acc);
+    const __m512i c = _mm512_maskz_compress_epi32(acc, v);
+    const __m512i r = _mm512_permutexvar_epi32(rev, c);
+    _mm512_mask_storeu_epi32((void*)(j + (int64_t)ii - 15), (__mmask16)(0xFFFFu << (16 - cnt)),
+                             r);
+    ii -= (uint32_t)cnt;
+    k += 16;
+  }
+  i = ii;
+  return k;
+}
+
+bool has_avx512() {
+  static const bool yes = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512vl");
+  return yes;
+}
+
 // Fisher-Yates targets of `count` successive permutations of arange(n): j[c][i] for
 // i = n-1 .. 1 (j[c][0] = 0), the draw/accept state machine of numpy's random_interval with the
 // accept step branch-free (the draw is always stored; i only advances on acceptance).
@@ -92,6 +131,7 @@ inline uint32_t smear(uint32_t m) {
 // with no exit test: i falls by at most one per draw, so it cannot leave the band early.
 void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
   int opos = g.pos;
+  const bool simd = has_avx512();
   for (int32_t c = 0; c < count; ++c) {
     int32_t* __restrict j = out + (int64_t)c * n;
     if (n > 0) j[0] = 0;
@@ -104,9 +144,14 @@ void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
           twist_block(g.mt, g.out);
           opos = 0;
         }
+        if (simd && i >= lo + 15) {
+          opos += (int)draw_groups_avx512(g.out + opos, (uint32_t)(kN - opos), mask, i, lo, j);
+          if (opos >= kN || i < lo) continue;
+        }
         const uint32_t* __restrict o = g.out + opos;
         const uint32_t left = (uint32_t)(kN - opos);
-        const uint32_t run = left < i - lo + 1 ? left : i - lo + 1;
+        uint32_t run = left < i - lo + 1 ? left : i - lo + 1;
+        if (simd && run > 16) run = 16;  // one group by the serial chain, then SIMD again
         for (uint32_t k = 0; k < run; ++k) {
           const uint32_t v = o[k] & mask;
           j[i] = (int32_t)v;
