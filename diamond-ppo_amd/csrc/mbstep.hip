@@ -44,6 +44,7 @@ constexpr int NSB = S / 16;                             // 16-sample MFMA tiles 
 constexpr int NPASS = S / (kTeamWaves * 8);             // gather/head passes (8 lanes/sample)
 constexpr int SPW = S / kTeamWaves;                     // samples per wave in the head phases
 static_assert(NPASS == 1, "one gather/head pass per step");
+static_assert(S == 32, "wgrad16 maps its 8 k-steps x 4 lane groups onto 32 samples");
 constexpr int SA = 68;                                  // stride of 64-col images
 constexpr int SAC = 132;                                // stride of the [ha | hc] images
 constexpr int SD = 68;                                  // stride of the per-sample head image
@@ -147,6 +148,20 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Sum over each aligned group of 8 lanes, the result in all 8 lanes, with DPP lane moves (VALU
+// operand modifiers) instead of ds_bpermute round trips through the LDS unit.  The adds pair
+// lanes exactly as x += shfl_xor(x, 1); x += shfl_xor(x, 2); x += shfl_xor(x, 4) would.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8(float x) {
+  x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]: lane ^ 1
+  x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]: lane ^ 2
+  x += dpp_mov<0x141>(x);  // row_half_mirror: lane 7 - i of the 8-lane group (the other quad)
+  return x;
+}
+
 __device__ __forceinline__ float tanh_f(float x) {
   // tanh via one exp and one hardware reciprocal, branch-free: t = e^{-2|x|},
   // tanh = sign(x) (1 - t) / (1 + t).  Absolute error <= ~1.5e-7 over the whole range (1 - t
@@ -243,7 +258,7 @@ __device__ __forceinline__ void tanh_rows(f32x4 (&v)[NSB]) {
 }
 
 // dW rows (16q..) += sum over the S staged samples: A = dZ image (cols perm(o)), B = X image
-// (k = sample).  Operands are prefetched two sample-quads ahead of their MFMAs.
+// (k = sample).  Operands are prefetched two k-steps ahead of their MFMAs.
 template <int NIB>
 __device__ __forceinline__ void wgrad16(f32x4* acc, const float* DZ, int dz_stride,
                                         int dz_col0, const float* X, int x_stride, int x_col0,
@@ -255,8 +270,11 @@ __device__ __forceinline__ void wgrad16(f32x4* acc, const float* DZ, int dz_stri
   constexpr int PD = 2;  // prefetch distance
   const int ca = dz_col0 + perm(row0 + l15);
   float av[PD + 1], bv[PD + 1][NIB];
+  // k-step t of lane group h4 takes sample (t & 3) + 4 h4 + 16 (t >> 2): any bijection onto the
+  // step's samples sums the same terms, and this one puts lane groups h4 and h4 + 1 four rows
+  // apart, i.e. 16 banks apart at every image stride used (== 4 mod 32): conflict-free b32 reads
   auto load = [&](int t, int slot) {
-    const int s = 4 * t + h4;
+    const int s = (t & 3) + 4 * h4 + 16 * (t >> 2);
     av[slot] = DZ[s * dz_stride + ca];
 #pragma unroll
     for (int ib = 0; ib < NIB; ++ib) bv[slot][ib] = X[s * x_stride + x_col0 + perm(16 * ib + l15)];
@@ -473,9 +491,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) part += w1[j] * ha1[j];
           }
-          part += __shfl_xor(part, 1);
-          part += __shfl_xor(part, 2);
-          part += __shfl_xor(part, 4);
+          part = sum8(part);
           out[k] = part + lds[L.bo + k];
         }
         float vp = 0.f;
@@ -493,9 +509,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) vp += w1[j] * hc1[j];
         }
-        vp += __shfl_xor(vp, 1);
-        vp += __shfl_xor(vp, 2);
-        vp += __shfl_xor(vp, 4);
+        vp = sum8(vp);
         const float v = vp + lds[L.bv];
         const float adv = sc[2], ret = sc[3];
         float logp = 0.f, ent = 0.f;
