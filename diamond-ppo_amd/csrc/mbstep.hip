@@ -59,6 +59,12 @@ constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;
 // wave arrives (its phase work issued and drained) and when the barrier releases it.
 constexpr int kTraceBars = 128;
 __device__ long long g_phase_trace[kTraceBars][kThreads / 64][2];
+__device__ long long g_heads_trace[kTraceBars][4];
+#define HEAD_STAMP(k)                                                                   \
+  do {                                                                                  \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && tr_k_ < kTraceBars)                     \
+      g_heads_trace[tr_k_][k] = __builtin_amdgcn_s_memtime();                          \
+  } while (0)
 #define STEP_BARRIER()                                                        \
   do {                                                                        \
     __builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0) only, as __syncthreads */ \
@@ -73,6 +79,9 @@ __device__ long long g_phase_trace[kTraceBars][kThreads / 64][2];
   } while (0)
 #else
 #define STEP_BARRIER() __syncthreads()
+#define HEAD_STAMP(k) \
+  do {                \
+  } while (0)
 #endif
 
 __host__ __device__ constexpr int perm(int k) { return (k & ~15) + 4 * (k & 3) + ((k >> 2) & 3); }
@@ -350,13 +359,13 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     const int hj = lane & 7;             // 8 lanes per sample
     const int hs = SPW * q + (lane >> 3);  // this lane group's sample within the step
 
-    // Sample-record prefetch, one step ahead in two stages so no phase waits on a dependent
-    // global round trip: the indices of step+1 are loaded after the gather, the record fields
-    // (observation chunk, {action, old log-prob, advantage, return}, continuous actions) after
-    // the heads; the head-gradient phase and the next layer phases cover their latency.
+    // Sample-record prefetch: after the heads of step it the records of step it+1 (observation
+    // chunk, {action, old log-prob, advantage, return}, continuous actions) and the indices of step
+    // it+2 are requested; the records are gathered at random (latency, not bandwidth).
     constexpr int NA4 = CONT ? (AMAX + 3) / 4 : 1;
     int nidx = 0;
-    f32x4 pobs, psc, pact[NA4];
+    f32x4 pobs, psc, pact[NA4];   // records of the next step (in flight)
+    f32x4 csc, cact[NA4];          // {action bits, old log-prob, adv, return} of the current step
     auto load_idx = [&](int it) {
       const int step = it * (int)gridDim.x + (int)blockIdx.x;
       const int si = step * S + hs;
@@ -386,6 +395,9 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     };
     load_idx(0);
     load_rec(0);
+    csc = psc;
+#pragma unroll
+    for (int c = 0; c < NA4; ++c) cact[c] = pact[c];
     gather(0);
     load_idx(1);
     __syncthreads();  // LDS head weights / biases and X0 of step 0 visible
@@ -468,7 +480,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       if (act) {
         const int si = step * S + hs;
         const bool valid = si < a.m;
-        const f32x4 sc = psc;  // {action bits, old logp, adv, return}
+        const f32x4 sc = csc;  // {action bits, old logp, adv, return}
         const float* hrow = HAC + hs * SAC;
         const f32x4 ha0 = *(const f32x4*)(hrow + 4 * hj), ha1 = *(const f32x4*)(hrow + 32 + 4 * hj);
         const f32x4 hc0 = *(const f32x4*)(hrow + 64 + 4 * hj);
@@ -511,6 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         }
         vp = sum8(vp);
         const float v = vp + lds[L.bv];
+        HEAD_STAMP(0);
         const float adv = sc[2], ret = sc[3];
         float logp = 0.f, ent = 0.f;
         float p[AMAX], lp[AMAX], xa[AMAX], sig[AMAX];
@@ -520,7 +533,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
             xa[k] = 0.f;
             sig[k] = 1.f;
             if (k < a.A) {
-              xa[k] = pact[k >> 2][k & 3];
+              xa[k] = cact[k >> 2][k & 3];
               sig[k] = __expf(lds[L.ls + k]);
               const float lsc = __logf(sig[k]);
               const float d = xa[k] - out[k];
@@ -551,6 +564,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
             }
           }
         }
+        HEAD_STAMP(1);
         const float ratio = __expf(logp - sc[1]);                        // ppo.py:266
         const float rcl = fminf(fmaxf(ratio, 1.0f - a.clip_eps), 1.0f + a.clip_eps);
         const float u = -adv * ratio, w = -adv * rcl;                    // ppo.py:267-269
@@ -585,8 +599,12 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
           }
         }
         if (hj == 0) drow[32] = dv;
+        HEAD_STAMP(2);
       }
+      // the next step's sample records (gathered in interval 5, heads of the next set) and the
+      // index after that
       load_rec(it + 1);
+      load_idx(it + 2);
       STEP_BARRIER();
       // ---- (5) head weight gradients (lane = feature column) and dZa, dZc of this wave's rows;
       // then the gather of step it+1 (its X0 buffer was last read by team 1 in interval 3)
@@ -639,7 +657,9 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         put_rows(DZAC, SAC, 64 + row0, dzc, l15, h4);
       }
       gather(it + 1);
-      load_idx(it + 2);
+      csc = psc;
+#pragma unroll
+      for (int c = 0; c < NA4; ++c) cact[c] = pact[c];
       STEP_BARRIER();
     }
 
@@ -808,6 +828,11 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #ifdef DPPO_PHASE_TRACE
 extern "C" __attribute__((visibility("default"))) int dppo_debug_phase_trace(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_trace), sizeof(g_phase_trace)) == hipSuccess
+             ? 0
+             : -2;
+}
+extern "C" __attribute__((visibility("default"))) int dppo_debug_heads_trace(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_heads_trace), sizeof(g_heads_trace)) == hipSuccess
              ? 0
              : -2;
 }

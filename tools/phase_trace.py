@@ -74,6 +74,21 @@ def main():
         print(f"{i:>3} {NAMES0[i]:>22} {w0:8.0f} {NAMES1[i]:>10} {w1:8.0f} {sp:9.0f}")
     print(f"set total {tot:.0f} cycles; whole launch {rel[nbar - 1].max() - rel[0].min():.0f} "
           f"cycles from first to last barrier")
+    if hasattr(h.lib, "dppo_debug_heads_trace"):
+        hb = np.zeros((128, 4), np.int64)
+        f2 = h.lib.dppo_debug_heads_trace
+        f2.argtypes = [ctypes.c_void_p]
+        assert f2(hb.ctypes.data) == 0
+        d = []
+        for k in steady:
+            if k % NI == 3 and hb[k, 0]:
+                start = rel[k - 1, 0]  # wave 0's release from the previous barrier
+                d.append((hb[k, 0] - start, hb[k, 1] - hb[k, 0], hb[k, 2] - hb[k, 1],
+                          arr[k, 0] - hb[k, 2]))
+        if d:
+            m = np.mean(np.array(d), axis=0)
+            print(f"heads+loss, wave 0: dots {m[0]:.0f}, softmax/logp {m[1]:.0f}, "
+                  f"ratio/grads/DOUT {m[2]:.0f}, to barrier {m[3]:.0f} cycles")
 
 
 if __name__ == "__main__":
