@@ -153,6 +153,18 @@ __device__ __forceinline__ float* opaque_base(float* p) {
   return p + z;
 }
 
+// Slab stores are write-through (sc1): the ~13 MB of per-workgroup gradient partials leave the
+// XCD L2s while the kernel runs instead of as dirty lines at the kernel boundary, and the reduce
+// kernel (other XCDs) reads them from memory either way (MI355X_MICROARCH.md: boundary,
+// publish-large).
+__device__ __forceinline__ void slab_put(float* p, float v) {
+#ifdef DPPO_ABL_PLAINSLAB
+  *p = v;
+#else
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -674,8 +686,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         vc += __shfl_xor(vc, off);
       }
       if (l15 == 0) {
-        slab[po.ba + row0 + 4 * h4 + r] = va;
-        slab[po.bc + row0 + 4 * h4 + r] = vc;
+        slab_put(slab + (po.ba + row0 + 4 * h4 + r), va);
+        slab_put(slab + (po.bc + row0 + 4 * h4 + r), vc);
       }
     }
     for (int off = 32; off >= 1; off >>= 1) {
@@ -698,15 +710,15 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       const float v = ((lds_[(0 * NH + e) * 64 + lane] + lds_[(1 * NH + e) * 64 + lane]) +
                        lds_[(2 * NH + e) * 64 + lane]) + lds_[(3 * NH + e) * 64 + lane];
       if (e < AMAX) {
-        if (e < a.A) slab[po.Wo + e * H + ftrue] = v;
+        if (e < a.A) slab_put(slab + (po.Wo + e * H + ftrue), v);
       } else if (e == AMAX) {
-        slab[po.Wv + ftrue] = v;
+        slab_put(slab + (po.Wv + ftrue), v);
       } else if (e == AMAX + 1) {
-        if (lane < a.A) slab[po.bo + lane] = v;
-        if (lane == 32) slab[po.bv] = v;
-        if (CONT && lane >= 33 && lane < 33 + a.A) slab[po.ls + (lane - 33)] = v;
+        if (lane < a.A) slab_put(slab + (po.bo + lane), v);
+        if (lane == 32) slab_put(slab + (po.bv), v);
+        if (CONT && lane >= 33 && lane < 33 + a.A) slab_put(slab + (po.ls + (lane - 33)), v);
       } else {
-        if (lane < 3) slab[a.p_total + lane] = v;
+        if (lane < 3) slab_put(slab + (a.p_total + lane), v);
       }
     }
   } else {
@@ -799,14 +811,14 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib) {
         const int i = 16 * ib + l15;
-        slab[po.W2 + o * H + i] = gW2[ib][r];
-        slab[po.Wa + o * H + i] = gWa[ib][r];
-        slab[po.Wc + o * H + i] = gWc[ib][r];
+        slab_put(slab + (po.W2 + o * H + i), gW2[ib][r]);
+        slab_put(slab + (po.Wa + o * H + i), gWa[ib][r]);
+        slab_put(slab + (po.Wc + o * H + i), gWc[ib][r]);
       }
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) {
         const int i = 16 * ib + l15;
-        if (i < a.D) slab[po.W1 + o * a.D + i] = gW1[ib][r];
+        if (i < a.D) slab_put(slab + (po.W1 + o * a.D + i), gW1[ib][r]);
       }
       float v1 = gb1[r], v2 = gb2[r];
 #pragma unroll
@@ -815,8 +827,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         v2 += __shfl_xor(v2, off);
       }
       if (l15 == 0) {
-        slab[po.b1 + o] = v1;
-        slab[po.b2 + o] = v2;
+        slab_put(slab + (po.b1 + o), v1);
+        slab_put(slab + (po.b2 + o), v2);
       }
     }
     __syncthreads();  // pairs with the forward team's head-partial rendezvous
