@@ -144,14 +144,20 @@ __global__ __launch_bounds__(kThreads) void gae_kernel(
 // and b + 8 (one XCD under round-robin dispatch) taking the two halves of the same 128-B lines
 // (speed only).  The serial recurrence is the latency floor, so a workgroup scans ALL its envs in
 // one pass: lanes are free, the 128 dependent steps are not.  9 waves per workgroup:
-//  * waves 0..7 each own one 16-step chunk of the current 128-step super-chunk.  An owner loads
+//  * waves 0..7 each own one 16-step chunk of the current 128-step super-chunk (wave w chunk
+//    7 - w: waves issue roughly in wave order, so the chunk the scan needs first is requested
+//    first; measured 0.4-0.6 us better than wave w -> chunk w at N = 8192).  An owner loads
 //    its chunk (16-B loads along the env axis), computes every term of the recurrence that does
 //    not depend on the carried advantage -- delta = (r + (gamma*nv)*nt) - v and
 //    coef = (c*nt)*ntr, the reference's op order -- and writes them env-major into LDS, flags the
 //    chunk, waits until the scan has passed it, then stores advantages and returns = v + a
 //    (16-B stores) and accumulates the normalisation statistics;
 //  * wave 8 is the scan (lane = env): per chunk 8 ds_read_b128, then 16 dependent steps of
-//    a = delta + coef * a (two VALU ops each), 4 ds_write_b128.
+//    a = delta + coef * a (two VALU ops each), 4 ds_write_b128; fully unrolled over the 8 chunks
+//    so the chain waits only for its own chunk's reads (1.2 us faster than the rolled loop, whose
+//    loop-carried register copies made every chunk wait for the next chunk's prefetch).
+// Timing-only builds: DPPO_GAE_TRACE (hand-off timeline, tools/gae_trace.py), DPPO_GAE_NOSCAN
+// (no recurrence: the movement-only time of this structure, wrong results).
 // An owner that has stored its chunk of tile i goes straight on to its chunk of tile i + 1, so
 // the chunks the scan reaches first (latest in time) start loading the next tile while the
 // scan is still walking back through the current one: loads and stores of different tiles
@@ -187,7 +193,6 @@ struct PipeLds {
   double wsum[kPChunks][2];
   int loaded[kPChunks];
   int scanned[kPChunks];
-  int issued[kPChunks];
 };
 
 __device__ __forceinline__ void gae_terms(float r, float v, float nv, float te, float tr, float g,
@@ -224,7 +229,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ val,
     const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
-    double* __restrict__ partials, int T, int N, float g, float c, int ordered) {
+    double* __restrict__ partials, int T, int N, float g, float c) {
   __shared__ __attribute__((aligned(16))) PipeLds<E> L;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ntiles = N / E;
@@ -232,7 +237,6 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
   if (threadIdx.x < kPChunks) {
     L.loaded[threadIdx.x] = 0;
     L.scanned[threadIdx.x] = 0;
-    L.issued[threadIdx.x] = 0;
   }
   __syncthreads();
   GAE_STAMP(0);
@@ -241,7 +245,9 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     constexpr int V4 = E / 4;              // lanes per row (4 envs each)
     constexpr int RP = kWave / V4;         // rows per pass
     constexpr int PER = kPChunk / RP;      // passes per chunk (2 for E = 32, 1 for E = 16)
-    const int k = wave;
+    // wave w owns chunk 7 - w: waves issue roughly in wave order, so the chunk the scan needs
+    // first (latest in time) is requested first and tends to land first
+    const int k = kPChunks - 1 - wave;
     const int e0 = 4 * (lane % V4);
     double lsum = 0.0, lsq = 0.0;
     int gen = 0;
@@ -253,13 +259,8 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
         const int lo = hi > kPSuper ? hi - kPSuper : 0;
         const int r0 = k * kPChunk;
         const int nr = min(kPChunk, hi - lo - r0);
-        // chunks issue their loads latest-in-time first, the order the scan consumes them
-        if (ordered && k + 1 < kPChunks) wait_flag(&L.issued[k + 1], gen);
-        if (nr <= 0) {  // no such chunk in this super-chunk: the scan skips it too
-          if (lane == 0) __hip_atomic_store(&L.issued[k], gen, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-          continue;
-        }
+        // (nr <= 0: no such chunk in this super-chunk -- it is written as identity rows, so the
+        // scan always walks all kPChunks chunks and can be fully unrolled)
         f32x4 xr[PER], xv[PER], xn[PER];
         uint32_t xt[PER], xu[PER];
 #pragma unroll
@@ -275,8 +276,6 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (lane == 0)
-          __hip_atomic_store(&L.issued[k], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
           const int row = p * RP + lane / V4;
@@ -333,61 +332,57 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
       L.wsum[k][1] = lsq;
     }
   } else if (lane < E) {
-    // ---------------- the scan, one lane per env, always whole 16-row chunks (see the padding)
+    // ---------------- the scan, one lane per env, all kPChunks chunks of every super-chunk
+    // (missing ones are identity rows), fully unrolled: the operands of chunk k sit in one of two
+    // static register sets while chunk k-1's are read into the other, so the chain waits only
+    // for its own chunk's LDS reads.
     const int e = lane;
     int gen = 0;
     for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
       float a = 0.0f;  // advantage carried backwards, 0 after the last step (ppo.py:198)
       for (int s = 0; s < nsup; ++s) {
         ++gen;
-        const int hi = T - s * kPSuper;
-        const int lo = hi > kPSuper ? hi - kPSuper : 0;
-        int k = (hi - lo + kPChunk - 1) / kPChunk - 1;
-        f32x4 d[4], cf[4];
-        wait_flag(&L.loaded[k], gen);
+        f32x4 d[2][4], cf[2][4];
+        wait_flag(&L.loaded[kPChunks - 1], gen);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          d[q] = *(const f32x4*)&L.delta[e][k * kPChunk + 4 * q];
-          cf[q] = *(const f32x4*)&L.coef[e][k * kPChunk + 4 * q];
+          d[(kPChunks - 1) & 1][q] = *(const f32x4*)&L.delta[e][(kPChunks - 1) * kPChunk + 4 * q];
+          cf[(kPChunks - 1) & 1][q] = *(const f32x4*)&L.coef[e][(kPChunks - 1) * kPChunk + 4 * q];
         }
-        for (; k >= 0; --k) {
+#pragma unroll
+        for (int k = kPChunks - 1; k >= 0; --k) {
+          const int b = k & 1;
           GAE_STAMP(25 + k);
           // speculative prefetch of chunk k-1: its flag is read before its data (LDS operations of
           // one wave complete in order), so a set flag proves the prefetched data is current
           int pf = gen;
-          f32x4 nd[4], ncf[4];
           if (k > 0) {
             pf = __hip_atomic_load(&L.loaded[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              nd[q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
-              ncf[q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
+              d[b ^ 1][q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
+              cf[b ^ 1][q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
             }
           }
+#ifndef DPPO_GAE_NOSCAN
           f32x4 av[4];
 #pragma unroll
           for (int j = kPChunk - 1; j >= 0; --j) {
-            a = gae_carry(d[j >> 2][j & 3], cf[j >> 2][j & 3], a);
+            a = gae_carry(d[b][j >> 2][j & 3], cf[b][j >> 2][j & 3], a);
             av[j >> 2][j & 3] = a;
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][k * kPChunk + 4 * q] = av[q];
+#endif
           if (lane == 0) set_flag(&L.scanned[k], gen);
           GAE_STAMP(33 + k);
-          if (k > 0) {
-            if (pf < gen) {
-              wait_flag(&L.loaded[k - 1], gen);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                nd[q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
-                ncf[q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
-              }
-            }
+          if (k > 0 && pf < gen) {
+            wait_flag(&L.loaded[k - 1], gen);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              d[q] = nd[q];
-              cf[q] = ncf[q];
+              d[b ^ 1][q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
+              cf[b ^ 1][q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
             }
           }
         }
@@ -529,8 +524,6 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
                    ((uintptr_t)tr % 16 == 0);
   // DPPO_GAE_STAGED=1 selects the earlier stage-all / scan / store-all kernel (A/B timing only)
   static const bool staged = std::getenv("DPPO_GAE_STAGED") != nullptr;
-  // DPPO_GAE_UNORDERED=1: chunk owners issue their loads without the latest-first order (A/B)
-  static const int ordered = std::getenv("DPPO_GAE_UNORDERED") == nullptr ? 1 : 0;
   if (vec && !staged) {
     // persistent: at most one workgroup per CU, a multiple of 16 so XCD pairs stay aligned
     static int cus = 0;
@@ -552,10 +545,10 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     *n_partials = grid;
     if (e32)
       DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                         adv, ret, partials, T, N, gamma, c, ordered);
+                  adv, ret, partials, T, N, gamma, c);
     else
       DPPO_LAUNCH(gae_pipe_kernel<16>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                         adv, ret, partials, T, N, gamma, c, ordered);
+                  adv, ret, partials, T, N, gamma, c);
   } else if (vec)
     DPPO_LAUNCH(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
                        partials, T, N, gamma, c);

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("DPPO_LIB", os.path.join(_HERE, "libdppo.so"))
+LIB_PATH = os.environ.get("DPPO_LIB") or os.path.join(_HERE, "libdppo.so")
 
 DPPO_OK = 0
 DPPO_EINVAL = -1
