@@ -8,9 +8,10 @@
 //
 // Both kernels are latency-bound, not bandwidth-bound (the slabs are G x P floats, ~13 MB at
 // G = 256; P ~ 13-14 K), so every thread keeps many independent loads in flight:
-//  * slab_reduce: one workgroup per 64 parameters; each of its 4 waves sums a quarter of the
-//    slabs for the 64 parameters (lane = parameter, 256 contiguous bytes per wave load, 16 loads
-//    in flight per lane), the four quarters are combined through LDS in a fixed order
+//  * slab_reduce: one workgroup per 64 parameters; each of its 16 waves sums every 16th slab
+//    for the 64 parameters (lane = parameter, 256 contiguous bytes per wave load, all 16 of a
+//    wave's loads in flight at once at G = 256: one memory round trip instead of the four a
+//    4-wave block needs), the 16 partials are combined through LDS in a fixed order
 //    (bit-reproducible), and each block also emits its partial sum of squares.
 //  * clip_adam: the global norm comes from those per-block partials (fixed order) or, after an
 //    RCCL all-reduce changed the gradient, from the gradient itself with 8 loads in flight.
@@ -20,35 +21,48 @@ namespace dppo {
 namespace {
 
 constexpr int kRedParams = 64;  // parameters per slab_reduce workgroup
+constexpr int kRedWaves = 16;
+constexpr int kRedThreads = kRedWaves * 64;
 
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slabs, int G,
-                                                          int64_t stride, int64_t p_total,
-                                                          float* __restrict__ grad,
-                                                          double* __restrict__ sq_part,
-                                                          int64_t ls_off, int ls_n, float ent_coef,
-                                                          int add_entropy_const) {
-  __shared__ float part[4][kRedParams];
+// Sum of slabs[g][p] over g for this block's 64 parameters (lane = parameter): wave w takes slabs
+// w, w + 16, ... in order, 16 loads in flight; the 16 wave partials are combined by wave 0 in
+// wave order.  Returns the total in wave 0 (other waves: 0).
+__device__ __forceinline__ float slab_sum(const float* __restrict__ slabs, int G, int64_t stride,
+                                          int64_t p, int64_t n, float (*part)[kRedParams]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
-  const int64_t n = p_total + 8;
   float s = 0.0f;
   if (p < n) {
     const float* src = slabs + p;
     int g = wave;
-    // 16 independent loads per batch (slabs wave, wave+4, ...), summed in slab order
-    for (; g + 60 < G; g += 64) {
-      float v[16];
+    for (; g + 15 * kRedWaves < G; g += 16 * kRedWaves) {
+      float x[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v[k] = src[(int64_t)(g + 4 * k) * stride];
+      for (int k = 0; k < 16; ++k) x[k] = src[(int64_t)(g + kRedWaves * k) * stride];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += v[k];
+      for (int k = 0; k < 16; ++k) s += x[k];
     }
-    for (; g < G; g += 4) s += src[(int64_t)g * stride];
+    for (; g < G; g += kRedWaves) s += src[(int64_t)g * stride];
   }
   part[wave][lane] = s;
   __syncthreads();
+  float t = 0.0f;
   if (wave == 0) {
-    float t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+#pragma unroll
+    for (int w = 0; w < kRedWaves; ++w) t += part[w][lane];
+  }
+  return t;
+}
+
+__global__ __launch_bounds__(kRedThreads) void slab_reduce_kernel(
+    const float* __restrict__ slabs, int G, int64_t stride, int64_t p_total,
+    float* __restrict__ grad, double* __restrict__ sq_part, int64_t ls_off, int ls_n,
+    float ent_coef, int add_entropy_const) {
+  __shared__ float part[kRedWaves][kRedParams];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
+  const int64_t n = p_total + 8;
+  float t = slab_sum(slabs, G, stride, p, n, part);
+  if (wave == 0) {
     // d(-beta * mean H)/d log_std = -beta per action dim (continuous_ppo.py:286-291): a
     // constant the per-sample kernel does not see; added once (rank 0 under data parallelism).
     if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
@@ -107,11 +121,12 @@ __device__ __forceinline__ float clip_coef(double sumsq, float max_norm, float* 
   return coef < 1.0f ? coef : 1.0f;
 }
 
-__device__ __forceinline__ void write_trace(float* trace, const float* grad, int64_t n, float norm,
-                                            float inv_m, float vf, float ent) {
-  const float lpi = grad[n + 0] * inv_m;
-  const float lv = grad[n + 1] * inv_m;
-  const float h = grad[n + 2] * inv_m;
+// s_pi, s_v, s_h: the loss slots {sum l_pi, sum l_v, sum H} that follow the gradient
+__device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v, float s_h,
+                                            float norm, float inv_m, float vf, float ent) {
+  const float lpi = s_pi * inv_m;
+  const float lv = s_v * inv_m;
+  const float h = s_h * inv_m;
   trace[0] = lpi + vf * lv - ent * h;  // ppo.py:276-280
   trace[1] = lpi;
   trace[2] = lv;
@@ -152,7 +167,7 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
     adam_elem(params, grad, m, v, k, coef, w1, w2, beta2, bc2_sqrt, eps, neg_step_size);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (out_norm) *out_norm = norm;
-    if (trace) write_trace(trace, grad, n, norm, inv_m, vf, ent);
+    if (trace) write_trace(trace, grad[n], grad[n + 1], grad[n + 2], norm, inv_m, vf, ent);
   }
 }
 
@@ -162,45 +177,29 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
 // arrival count (a monotonic counter: launch `epoch` waits for epoch x gridDim arrivals, so it is
 // never reset), each acquires (agent scope), sums the per-block squares in a fixed order and
 // applies Adam to its own 64 parameters, whose gradients it still holds in registers and whose
-// moments it prefetched before the wait.  The grid (~210 blocks of 256 threads) is always
+// moments it prefetched before the wait.  The grid (~210 blocks of 1024 threads) is always
 // resident; the wait is bounded.  (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
 // price list: fanin vs boundary.)
-__global__ __launch_bounds__(256) void reduce_adam_kernel(
+__global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     const float* __restrict__ slabs, int G, int64_t stride, int64_t p_total, float* grad,
     double* sq_part, int64_t ls_off, int ls_n, float ent_coef, int add_entropy_const,
     unsigned* arrivals, unsigned epoch, float* __restrict__ params, float* __restrict__ m,
     float* __restrict__ v, float max_norm, float neg_step_size, float bc2_sqrt, float beta1,
     float beta2, float eps, float* __restrict__ trace, float inv_m, float vf, float ent) {
 #pragma clang fp contract(off)
-  __shared__ float part[4][kRedParams];
+  __shared__ float part[kRedWaves][kRedParams];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
   const int64_t n = p_total + 8;
-  float s = 0.0f;
-  if (p < n) {
-    const float* src = slabs + p;
-    int g = wave;
-    for (; g + 60 < G; g += 64) {
-      float x[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = src[(int64_t)(g + 4 * k) * stride];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) s += x[k];
-    }
-    for (; g < G; g += 4) s += src[(int64_t)g * stride];
-  }
-  part[wave][lane] = s;
-  // this block's Adam operands, loaded while the other blocks finish
+  // this block's Adam operands, loaded while the slabs stream in
   float mk = 0.f, vk = 0.f, pk = 0.f;
   if (wave == 0 && p < p_total) {
     mk = m[p];
     vk = v[p];
     pk = params[p];
   }
-  __syncthreads();
-  float t = 0.f;
+  float t = slab_sum(slabs, G, stride, p, n, part);
   if (wave == 0) {
-    t = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
     if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
     if (p < n) __hip_atomic_store(grad + p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     double q = (p < p_total) ? (double)t * (double)t : 0.0;
@@ -219,14 +218,21 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(
       if (spins > (1 << 22)) break;  // never expected: the grid is resident
       __builtin_amdgcn_s_sleep(1);
     }
+#ifdef DPPO_ABL_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
   }
   __syncthreads();
   if (wave != 0) return;
+  // Everything read below that other blocks wrote (sq_part, the loss slots) is read with sc1
+  // (agent-scope atomic) loads, so no acquire fence (and its L1 invalidate, ~1.5 us per CU) is
+  // needed: producer sc1 stores -> vmcnt(0) -> arrival; consumer sees the count -> sc1 loads
+  // (cdna_hip_programming.md Guideline 16 R1, condition 4).
   // global norm: every block sums the same per-block squares in the same order
   double sq = 0.0;
-  for (int k = lane; k < (int)gridDim.x; k += 64) sq += sq_part[k];
+  for (int k = lane; k < (int)gridDim.x; k += 64)
+    sq += __hip_atomic_load(sq_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
   float norm;
   const float coef = clip_coef(sq, max_norm, &norm);
@@ -238,7 +244,12 @@ __global__ __launch_bounds__(256) void reduce_adam_kernel(
     v[p] = vk;
   }
   // the loss slots (published by the block past the last parameter) for the trace
-  if (blockIdx.x == 0 && lane == 0 && trace) write_trace(trace, grad, p_total, norm, inv_m, vf, ent);
+  if (blockIdx.x == 0 && lane == 0 && trace) {
+    const float s_pi = __hip_atomic_load(grad + p_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float s_v = __hip_atomic_load(grad + p_total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const float s_h = __hip_atomic_load(grad + p_total + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    write_trace(trace, s_pi, s_v, s_h, norm, inv_m, vf, ent);
+  }
 }
 
 }  // namespace
@@ -248,7 +259,7 @@ int slab_reduce_blocks(int64_t p_total) { return (int)((p_total + 8 + kRedParams
 int launch_slab_reduce(const float* slabs, int G, int64_t slab_stride, int64_t p_total,
                        float* grad, double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
                        int add_entropy_const, hipStream_t s) {
-  DPPO_LAUNCH(slab_reduce_kernel, dim3(slab_reduce_blocks(p_total)), dim3(256), 0, s,
+  DPPO_LAUNCH(slab_reduce_kernel, dim3(slab_reduce_blocks(p_total)), dim3(kRedThreads), 0, s,
                      slabs, G, slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef,
                      add_entropy_const);
   DPPO_LAUNCH_CHECK();
@@ -275,7 +286,7 @@ int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
                        float ent, hipStream_t s) {
-  DPPO_LAUNCH(reduce_adam_kernel, dim3(slab_reduce_blocks(p_total)), dim3(256), 0, s, slabs, G,
+  DPPO_LAUNCH(reduce_adam_kernel, dim3(slab_reduce_blocks(p_total)), dim3(kRedThreads), 0, s, slabs, G,
               slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef, add_entropy_const,
               arrivals, epoch, params, m, v, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
               trace, inv_m, vf, ent);
