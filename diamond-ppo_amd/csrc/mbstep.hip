@@ -49,6 +49,7 @@ constexpr int SA = 68;                                  // stride of 64-col imag
 constexpr int SAC = 132;                                // stride of the [ha | hc] images
 constexpr int SD = 68;                                  // stride of the per-sample head image
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+constexpr float kLn2 = 0.69314718055994530942f;
 constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;
 
 // Timing-only ablation switches (tools/ablate.py); a shipped build defines none of them.
@@ -181,6 +182,14 @@ __device__ __forceinline__ float sum8(float x) {
   x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]: lane ^ 2
   x += dpp_mov<0x141>(x);  // row_half_mirror: lane 7 - i of the 8-lane group (the other quad)
   return x;
+}
+
+// 8-term dot product as a balanced tree (3 dependent adds instead of 8): the head phase is a
+// latency chain, not a throughput one
+__device__ __forceinline__ float dot8(f32x4 w0, f32x4 w1, f32x4 x0, f32x4 x1) {
+  const float a = w0[0] * x0[0] + w0[1] * x0[1], b = w0[2] * x0[2] + w0[3] * x0[3];
+  const float c = w1[0] * x1[0] + w1[1] * x1[1], d = w1[2] * x1[2] + w1[3] * x1[3];
+  return (a + b) + (c + d);
 }
 
 __device__ __forceinline__ float tanh_f(float x) {
@@ -510,10 +519,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
               w0 = *(const f32x4*)(lds + L.Wo + k * H + 4 * hj);
               w1 = *(const f32x4*)(lds + L.Wo + k * H + 32 + 4 * hj);
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) part += w0[j] * ha0[j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) part += w1[j] * ha1[j];
+            part = dot8(w0, w1, ha0, ha1);
           }
           part = sum8(part);
           out[k] = part + lds[L.bo + k];
@@ -528,10 +534,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
             w0 = *(const f32x4*)(lds + L.Wv + 4 * hj);
             w1 = *(const f32x4*)(lds + L.Wv + 32 + 4 * hj);
           }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) vp += w0[j] * hc0[j];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) vp += w1[j] * hc1[j];
+          vp = dot8(w0, w1, hc0, hc1);
         }
         vp = sum8(vp);
         const float v = vp + lds[L.bv];
@@ -563,7 +566,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #pragma unroll
           for (int k = 0; k < AMAX; ++k)
             if (k < a.A) se += __expf(out[k] - mx);
-          const float lse = mx + __logf(se);
+          // se >= 1 (its largest term is exp(0)): the bare v_log_f32 (log2) needs no range fix-up
+          const float lse = mx + __builtin_amdgcn_logf(se) * kLn2;
 #pragma unroll
           for (int k = 0; k < AMAX; ++k) {
             lp[k] = 0.f;
