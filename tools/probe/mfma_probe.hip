@@ -1,0 +1,51 @@
+// Timing probe (not part of libdppo): issue rate of v_mfma_f32_16x16x4_f32 chains on gfx950.
+// Each wave runs `iters` rounds of NACC independent accumulator chains (operands in registers);
+// s_memtime brackets the loop.  Launch with 4 * waves_per_simd waves per workgroup, one workgroup
+// per CU, to see how two waves on a SIMD share the matrix pipe.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int NACC>
+__global__ __launch_bounds__(512) void mfma_chain(float* out, long long* cyc, int iters,
+                                                  int active_waves) {
+  const int wave = threadIdx.x >> 6;
+  f32x4 acc[NACC];
+  for (int i = 0; i < NACC; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, (float)threadIdx.x};
+  float a = 1.0f + threadIdx.x * 1e-3f, b = 0.5f;
+  long long t0 = __builtin_amdgcn_s_memtime();
+  if (wave < active_waves) {
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < NACC; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+    }
+  }
+  float s = 0.f;
+  for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][3];
+  long long t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if ((threadIdx.x & 63) == 0) {
+    cyc[blockIdx.x * 8 + wave] = t1 - t0;
+    if (blockIdx.x == 0) {  // absolute stamps of block 0 (overlap of its waves)
+      cyc[gridDim.x * 8 + 2 * wave] = t0;
+      cyc[gridDim.x * 8 + 2 * wave + 1] = t1;
+    }
+  }
+}
+
+extern "C" int probe_mfma(int nacc, float* out, long long* cyc, int iters, int waves,
+                          int active_waves, int blocks, void* stream) {
+  dim3 g(blocks), b(waves * 64);
+  hipStream_t s = (hipStream_t)stream;
+  switch (nacc) {
+    case 1: hipLaunchKernelGGL(mfma_chain<1>, g, b, 0, s, out, cyc, iters, active_waves); break;
+    case 2: hipLaunchKernelGGL(mfma_chain<2>, g, b, 0, s, out, cyc, iters, active_waves); break;
+    case 4: hipLaunchKernelGGL(mfma_chain<4>, g, b, 0, s, out, cyc, iters, active_waves); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
