@@ -5,6 +5,14 @@ state-independent ``actor_log_std`` parameter (:50-111; registered first, so it 
 entry of ``parameters()``), init without the small-output-layer scaling (:114-121).  The fused
 kernels evaluate the unsquashed JointNormal exactly as the reference does (there is no tanh squash
 anywhere in the reference: continuous_ppo.py:83-111,276-277).
+
+``ContinuousPPOConfig.tanh_squash`` (default False, an extension beyond the reference; SURVEY §8
+f2) makes ``rollout()`` send ``a = tanh(u)`` -- rescaled to the action space's bounds when they
+are finite -- to the environment while the experience keeps the Gaussian sample ``u``.  The
+squashed policy's log-density is ``log N(u) - sum log(1 - tanh(u)^2)`` (:func:`squashed_log_prob`);
+the correction does not depend on the parameters, so it cancels in the PPO ratio and the update
+is exactly the unsquashed Gaussian update on ``u`` -- the same fused kernels, no second path.  The
+entropy bonus stays the Gaussian one (the squashed entropy has no closed form).
 """
 from __future__ import annotations
 
@@ -43,6 +51,7 @@ class ContinuousPPOConfig:
     save_interval: float = 600
     verbose: bool = True
     device_index: int = 0
+    tanh_squash: bool = False  # extension: env actions tanh(u), experience keeps u (module doc)
 
 
 class JointNormal(torch.distributions.Normal):
@@ -92,6 +101,25 @@ class ContinuousActorCriticNetwork(nn.Module):
         return mean, log_std, self.critic_head(x).squeeze(-1)
 
 
+def squashed_log_prob(mean: torch.Tensor, log_std: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """log-density of a = tanh(u), u ~ N(mean, exp(log_std)), summed over action dims:
+    log N(u) - sum log(1 - tanh(u)^2), with log(1 - tanh(u)^2) = 2 (log 2 - u - softplus(-2u))
+    (stable for large |u|)."""
+    base = JointNormal(loc=mean, scale=log_std.exp()).log_prob(u)
+    corr = 2.0 * (np.log(2.0) - u - torch.nn.functional.softplus(-2.0 * u))
+    return base - corr.sum(-1)
+
+
+def squash_to_space(u: np.ndarray, action_space) -> np.ndarray:
+    """tanh(u), rescaled to [low, high] of a Box with finite bounds (else left in [-1, 1])."""
+    a = np.tanh(u)
+    low = np.asarray(getattr(action_space, "low", -1.0), dtype=np.float64)
+    high = np.asarray(getattr(action_space, "high", 1.0), dtype=np.float64)
+    if np.all(np.isfinite(low)) and np.all(np.isfinite(high)):
+        a = low + (a + 1.0) * 0.5 * (high - low)
+    return a.astype(u.dtype, copy=False)
+
+
 def network_parameter_init_(network: nn.Module, gain: float = 1.0) -> None:
     """Orthogonal weights and zero biases, no output scaling (continuous_ppo.py:114-121)."""
     with torch.no_grad():
@@ -110,3 +138,8 @@ class ContinuousPPO(_AgentBase):
     def __init__(self, env_fn: Callable[[], Any], cfg: ContinuousPPOConfig = ContinuousPPOConfig(),
                  network_cls: Any = ContinuousActorCriticNetwork, envs=None) -> None:
         self._setup(env_fn, cfg, network_cls, envs)
+
+    def _env_actions(self, actions: np.ndarray) -> np.ndarray:
+        if getattr(self.cfg, "tanh_squash", False):
+            return squash_to_space(actions, self.envs.single_action_space)
+        return actions

@@ -142,6 +142,11 @@ class _AgentBase:
                              verbose=cfg.verbose and rank == 0)
         self.current_step = 0
 
+    def _env_actions(self, actions: np.ndarray) -> np.ndarray:
+        """What the environment receives for the sampled actions (identity; ContinuousPPO's
+        tanh_squash option overrides it).  The experience always keeps ``actions``."""
+        return actions
+
     # -- drop-in surface ------------------------------------------------------------------------
     def rollout(self) -> list[list[np.ndarray]]:
         """Collect one rollout across the vector env (reference ppo.py:153-186)."""
@@ -149,7 +154,8 @@ class _AgentBase:
         observations = self.current_observations
         for _ in range(self.cfg.rollout_steps):
             actions = self.network.get_actions(observations, device=self.device)
-            next_observations, rewards, terminations, truncations, infos = self.envs.step(actions)
+            next_observations, rewards, terminations, truncations, infos = self.envs.step(
+                self._env_actions(actions))
             experience.append([observations, next_observations, actions, rewards, terminations,
                                truncations])
             dones = np.logical_or(terminations, truncations)

@@ -350,3 +350,48 @@ def test_permutation_lookahead_hit_and_miss(device_shuffle):
     assert np.array_equal(p1, p2)
     assert np.array_equal(k1, k2) and q1 == q2
     assert hits1 == 2 and hits2 == 0
+
+
+# ---------------------------------------------------------------------------------------------
+def test_tanh_squash_rollout_and_learn():
+    """ContinuousPPOConfig.tanh_squash (extension): the env receives tanh(u) rescaled
+    to the Box bounds, the experience keeps the Gaussian sample u, and learn() on that experience
+    is bit-identical to the unsquashed agent's learn() on the same experience (the squash's
+    log-density correction does not depend on the parameters)."""
+    import gym_stub
+
+    class RecordingEnvs(gym_stub.SyncVectorEnv):
+        def step(self, actions):
+            self.sent.append(np.array(actions, copy=True))
+            return super().step(actions)
+
+    T, Nn, D, A = 8, 16, 5, 3
+    params = []
+    squashed_exp = None
+    for squash in (True, False):
+        np.random.seed(0)
+        torch.manual_seed(0)
+        envs = RecordingEnvs([lambda: gym_stub.SyntheticEnv(D, 1, continuous=True, act_dim=A)] * Nn)
+        envs.single_action_space.low = -2.0
+        envs.single_action_space.high = 2.0
+        envs.sent = []
+        cfg = diamond.ContinuousPPOConfig(rollout_steps=T, num_envs=Nn, verbose=False,
+                                          tanh_squash=squash)
+        agent = diamond.ContinuousPPO(None, cfg, envs=envs)
+        agent.current_observations, _ = envs.reset(seed=3)
+        exp = agent.rollout()
+        u = np.stack([e[2] for e in exp])
+        sent = np.stack(envs.sent)
+        if squash:
+            assert np.all(np.abs(sent) <= 2.0)
+            np.testing.assert_allclose(sent, (-2.0 + (np.tanh(u) + 1.0) * 2.0).astype(np.float32),
+                                       rtol=1e-6, atol=1e-6)
+            assert not np.allclose(sent, u)
+            squashed_exp = exp
+        else:
+            np.testing.assert_array_equal(sent, u)
+        np.random.seed(7)
+        agent.learn(squashed_exp)
+        torch.cuda.synchronize()
+        params.append(flat_params(agent))
+    np.testing.assert_array_equal(params[0], params[1])

@@ -18,6 +18,25 @@ def header_symbols():
     return sorted(set(re.findall(r"\b(dppo_[a-z0-9_]+)\s*\(", text)))
 
 
+def test_squashed_log_prob_change_of_variables():
+    """squashed_log_prob = log N(u) - sum log(1 - tanh(u)^2): stable form vs the naive one
+    (float64, moderate u), and the density of a = tanh(u) integrates to 1 (1-D, trapezoid)."""
+    from diamond.continuous_ppo import squashed_log_prob
+    g = torch.Generator().manual_seed(0)
+    mean = torch.randn(64, 3, generator=g, dtype=torch.float64)
+    log_std = (0.3 * torch.randn(1, 3, generator=g, dtype=torch.float64)).expand(64, 3)
+    u = mean + log_std.exp() * torch.randn(64, 3, generator=g, dtype=torch.float64)
+    naive = (torch.distributions.Normal(mean, log_std.exp()).log_prob(u)
+             - torch.log(1.0 - torch.tanh(u) ** 2)).sum(-1)
+    np.testing.assert_allclose(squashed_log_prob(mean, log_std, u).numpy(), naive.numpy(),
+                               rtol=1e-10, atol=1e-10)
+    a = torch.linspace(-0.999999, 0.999999, 200001, dtype=torch.float64)
+    uu = torch.atanh(a)[:, None]
+    dens = squashed_log_prob(torch.tensor([[0.3]], dtype=torch.float64),
+                             torch.tensor([[-0.2]], dtype=torch.float64), uu).exp()
+    assert abs(float(torch.trapezoid(dens, a)) - 1.0) < 1e-4
+
+
 def test_library_loads_and_exports_every_header_symbol():
     lib = N.load()
     syms = header_symbols()
