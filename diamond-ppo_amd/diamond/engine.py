@@ -173,6 +173,104 @@ def stage_experience(experience, device, continuous) -> DeviceRollout:
                          up(rewards, np.float32), up(terms, np.uint8), up(truncs, np.uint8))
 
 
+class RolloutStager:
+    """Per-step staging of a rollout into the SoA HBM buffer while the envs step.
+
+    ``put(t, ...)`` copies step t's arrays into row t of a pinned host slot and enqueues that
+    row's host->device copy on a side stream, so the PCIe transfer of a rollout overlaps the
+    environment stepping instead of following it (``stage_experience`` stacks and uploads the
+    whole rollout inside learn()).  Two slots alternate: a slot's pinned rows are rewritten only
+    after its previous copies completed (``end`` marks them), and its device buffers only after
+    the learn() that read them (``release``).  ``finish()`` returns the device rollout and makes
+    the caller's stream wait for the copies."""
+
+    def __init__(self, T: int, N: int, obs_shape, act_shape, continuous: bool, device):
+        self.T, self.N, self.device = T, N, device
+        self.continuous = bool(continuous)
+        D = int(np.prod(obs_shape))
+        A = int(np.prod(act_shape)) if continuous else 1
+        self.D, self.A = D, A
+        self.stream = torch.cuda.Stream(device=device)
+        self.slots = []
+        for _ in range(2):
+            host = {
+                "obs": torch.empty((T, N, D), dtype=torch.float32).pin_memory(),
+                "next_obs": torch.empty((T, N, D), dtype=torch.float32).pin_memory(),
+                "actions": (torch.empty((T, N, A), dtype=torch.float32) if continuous
+                            else torch.empty((T, N), dtype=torch.int32)).pin_memory(),
+                "rewards": torch.empty((T, N), dtype=torch.float32).pin_memory(),
+                "term": torch.empty((T, N), dtype=torch.uint8).pin_memory(),
+                "trunc": torch.empty((T, N), dtype=torch.uint8).pin_memory(),
+            }
+            dev = {k: torch.empty(v.shape, dtype=v.dtype, device=device) for k, v in host.items()}
+            self.slots.append({"host": host, "dev": dev, "copied": None, "released": None,
+                               "np": {k: v.numpy() for k, v in host.items()}})
+        self.cur = 1
+        self.rows = 0
+        self.flushed = 0
+        self.chunk = max(1, T // 8)  # rows per flush
+
+    def begin(self) -> None:
+        self.cur ^= 1
+        sl = self.slots[self.cur]
+        if sl["copied"] is not None:
+            sl["copied"].synchronize()           # the pinned rows are free again
+        if sl["released"] is not None:
+            self.stream.wait_event(sl["released"])  # the learn() that read the device rows is done
+        self.rows = 0
+        self.flushed = 0
+
+    def put(self, t: int, obs, next_obs, actions, rewards, term, trunc) -> None:
+        sl = self.slots[self.cur]
+        h = sl["np"]
+        h["obs"][t] = np.reshape(obs, (self.N, self.D))
+        h["next_obs"][t] = np.reshape(next_obs, (self.N, self.D))
+        if self.continuous:
+            h["actions"][t] = np.reshape(actions, (self.N, self.A))
+        else:
+            h["actions"][t] = actions
+        h["rewards"][t] = rewards
+        h["term"][t] = term
+        h["trunc"][t] = trunc
+        self.rows = t + 1
+        if self.rows - self.flushed >= self.chunk:
+            self._flush()
+
+    def _flush(self) -> None:
+        """Enqueue the host->device copies of the rows written since the last flush (one copy per
+        array: the per-call cost, not the bytes, dominates at rollout-row sizes)."""
+        sl = self.slots[self.cur]
+        r0, r1 = self.flushed, self.rows
+        if r1 > r0:
+            with torch.cuda.stream(self.stream):
+                for k, v in sl["host"].items():
+                    sl["dev"][k][r0:r1].copy_(v[r0:r1], non_blocking=True)
+        self.flushed = r1
+
+    def end(self) -> None:
+        """All rows written: flush the rest and mark the slot's copies (also when learn() never
+        claims them)."""
+        self._flush()
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        self.slots[self.cur]["copied"] = ev
+
+    def finish(self) -> "DeviceRollout":
+        if self.rows != self.T:
+            raise ValueError(f"staged {self.rows} of {self.T} rollout steps")
+        sl = self.slots[self.cur]
+        torch.cuda.current_stream(self.device).wait_event(sl["copied"])
+        d = sl["dev"]
+        return DeviceRollout(d["obs"], d["next_obs"], d["actions"], d["rewards"], d["term"],
+                             d["trunc"])
+
+    def release(self) -> None:
+        """Mark the current slot's device rows free once the work queued so far has run."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.slots[self.cur]["released"] = ev
+
+
 def hparams(cfg, lr: float, adam_step: int, betas=(0.9, 0.999)) -> N.HParams:
     return N.HParams(gamma=cfg.gamma, gae_lambda=cfg.gae_lambda, ppo_clip=cfg.ppo_clip,
                      value_loss_weight=cfg.value_loss_weight, entropy_beta=cfg.entropy_beta,

@@ -21,8 +21,8 @@ import torch.nn as nn
 
 from . import _native as N
 from ._spaces import is_box, is_discrete, make_vector_env
-from .engine import NativeLearner, DeviceRollout, dist_world, require_gpu, rebind_after_load, \
-    stage_experience
+from .engine import NativeLearner, DeviceRollout, RolloutStager, dist_world, require_gpu, \
+    rebind_after_load, stage_experience
 from .utils import Checkpointer, Logger, Ticker, Timer
 
 
@@ -107,6 +107,7 @@ class _AgentBase:
     continuous = False
     default_network: type = None
     init_fn = staticmethod(network_parameter_init_)
+    stage_rollout = True  # rollout() stages each step into HBM as the envs step (RolloutStager)
 
     def _setup(self, env_fn, cfg, network_cls, envs=None):
         self.device = require_gpu(getattr(cfg, "device_index", 0))
@@ -141,6 +142,8 @@ class _AgentBase:
         self.ticker = Ticker(cfg.total_steps, cfg.num_envs, cfg.rollout_steps,
                              verbose=cfg.verbose and rank == 0)
         self.current_step = 0
+        self._stager = None
+        self._staged = None
 
     def _env_actions(self, actions: np.ndarray) -> np.ndarray:
         """What the environment receives for the sampled actions (identity; ContinuousPPO's
@@ -149,22 +152,47 @@ class _AgentBase:
 
     # -- drop-in surface ------------------------------------------------------------------------
     def rollout(self) -> list[list[np.ndarray]]:
-        """Collect one rollout across the vector env (reference ppo.py:153-186)."""
+        """Collect one rollout across the vector env (reference ppo.py:153-186).  Each step is
+        also staged into the SoA HBM buffer on a side stream while the envs step; learn() of the
+        returned list then skips the stack-and-upload."""
         experience = []
         observations = self.current_observations
-        for _ in range(self.cfg.rollout_steps):
+        stager = self._rollout_stager()
+        if stager is not None:
+            stager.begin()
+        for t in range(self.cfg.rollout_steps):
             actions = self.network.get_actions(observations, device=self.device)
             next_observations, rewards, terminations, truncations, infos = self.envs.step(
                 self._env_actions(actions))
             experience.append([observations, next_observations, actions, rewards, terminations,
                                truncations])
+            if stager is not None:
+                stager.put(t, observations, next_observations, actions, rewards, terminations,
+                           truncations)
             dones = np.logical_or(terminations, truncations)
             observations, infos = (self.envs.reset(options={"reset_mask": dones})
                                    if np.any(dones) else (next_observations, infos))
             if self.ticker is not None:
                 self.ticker.tick(rewards, dones)
         self.current_observations = observations
+        if stager is not None:
+            stager.end()
+        # what was staged: the list and every array object in it (a list edited afterwards, or
+        # arrays replaced in it, is re-staged from its contents by learn(); arrays mutated IN
+        # PLACE after rollout() are not detected -- set ``agent.stage_rollout = False`` for that)
+        self._staged = ((experience, [id(a) for row in experience for a in row])
+                        if stager is not None else None)
         return experience
+
+    def _rollout_stager(self):
+        if not self.stage_rollout:
+            return None
+        if self._stager is None:
+            obs_shape = (self._obs_dim,)
+            act_shape = (self._act_dim,) if self.continuous else ()
+            self._stager = RolloutStager(self.cfg.rollout_steps, self.cfg.num_envs, obs_shape,
+                                         act_shape, self.continuous, self.device)
+        return self._stager
 
     def calculate_advantage(self, rewards, terminations, truncations, values, next_values):
         """GAE (reference ppo.py:188-222) on the gfx950 kernel, bit-exact with the reference's
@@ -201,6 +229,13 @@ class _AgentBase:
 
     def learn(self, experience: list[list[np.ndarray]]) -> None:
         """Update policy and value networks with one rollout (reference ppo.py:224-287)."""
+        staged, self._staged = self._staged, None
+        if (staged is not None and experience is staged[0]
+                and [id(a) for row in experience for a in row] == staged[1]):
+            ro = self._stager.finish()
+            self.learn_device(ro)
+            self._stager.release()
+            return
         ro = stage_experience(experience, self.device, self.continuous)
         self.learn_device(ro)
 

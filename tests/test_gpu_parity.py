@@ -395,3 +395,31 @@ def test_tanh_squash_rollout_and_learn():
         torch.cuda.synchronize()
         params.append(flat_params(agent))
     np.testing.assert_array_equal(params[0], params[1])
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_staged_rollout_learn_matches_unstaged(continuous):
+    """rollout() stages every step into HBM as the envs step (RolloutStager, SURVEY §8 f1);
+    learn() of the returned list must equal learn() of the same experience stacked and uploaded
+    the reference way -- also when the list handed to learn() is a different object (re-staged),
+    and across consecutive rollouts (the two staging slots alternate)."""
+    import gym_stub
+    T, Nn, D, A = 16, 32, 6, 3
+    results = []
+    for mode in ("staged", "unstaged", "copy"):
+        np.random.seed(0)
+        torch.manual_seed(0)
+        envs = gym_stub.SyncVectorEnv(
+            [lambda: gym_stub.SyntheticEnv(D, A, continuous=continuous, act_dim=A)] * Nn)
+        Cfg = diamond.ContinuousPPOConfig if continuous else diamond.PPOConfig
+        Agent = diamond.ContinuousPPO if continuous else diamond.PPO
+        agent = Agent(None, Cfg(rollout_steps=T, num_envs=Nn, verbose=False), envs=envs)
+        agent.stage_rollout = mode != "unstaged"
+        agent.current_observations, _ = envs.reset(seed=5)
+        for _ in range(3):
+            exp = agent.rollout()
+            agent.learn(list(exp) if mode == "copy" else exp)
+        torch.cuda.synchronize()
+        results.append(flat_params(agent))
+    np.testing.assert_array_equal(results[0], results[1])
+    np.testing.assert_array_equal(results[2], results[1])
