@@ -89,6 +89,8 @@ size_t mlp_lds_bytes_eval(const MlpShape& sh);
 int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                 const void* actions, const float* next_obs, float* logp, float* values,
                 float* next_values, int64_t n, hipStream_t s);
+int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
+               void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s);
 struct GradArgs {
   const float* params;
   const float* rec;

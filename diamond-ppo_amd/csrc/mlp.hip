@@ -333,6 +333,143 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Action sampling for the rollout (get_actions, ppo.py:73-82 / continuous_ppo.py:83-93): base +
+// actor forward, then Categorical(logits).sample() or Normal(mean, exp(log_std)).sample() on the
+// lane that holds the sample.  Randomness: Philox4x32-10 keyed by `seed`, counter (sample index,
+// call counter) -- a deterministic stream of its own (the reference draws from torch's generator:
+// same distribution, not the same draws).
+__device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+}
+
+__device__ __forceinline__ void philox4x32(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = mulhi32(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = mulhi32(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    c[0] = hi1 ^ c[1] ^ k0;
+    c[1] = lo1;
+    c[2] = hi0 ^ c[3] ^ k1;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// u32 -> uniform in (0, 1): 24 random bits, centred in their interval (never 0 or 1)
+__device__ __forceinline__ float u01(uint32_t x) {
+  return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+struct ActArgs {
+  LdsLayout L;
+  ParamOffsets po;
+  const float* params;
+  const float* obs;
+  void* actions;
+  int64_t n;
+  uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
+  int D, D8, nq1, A;
+};
+
+__device__ __forceinline__ void load_weights_actor(float* lds, const ActArgs& a, int tid) {
+  const float* P = a.params;
+  const LdsLayout& L = a.L;
+  for (int k = tid; k < H * L.S1; k += kThreads) {
+    const int o = k / L.S1, c = k % L.S1;
+    lds[L.W1 + k] = c < a.D ? P[a.po.W1 + o * a.D + c] : 0.0f;
+  }
+  for (int k = tid; k < H * H; k += kThreads) {
+    const int o = k >> 6, c = k & 63;
+    lds[L.W2 + o * SW + c] = P[a.po.W2 + k];
+    lds[L.Wa + o * SW + c] = P[a.po.Wa + k];
+  }
+  for (int k = tid; k < a.A * H; k += kThreads) lds[L.Wo + k] = P[a.po.Wo + k];
+  for (int k = tid; k < H; k += kThreads) {
+    lds[L.b1 + k] = P[a.po.b1 + k];
+    lds[L.b2 + k] = P[a.po.b2 + k];
+    lds[L.ba + k] = P[a.po.ba + k];
+  }
+  for (int k = tid; k < 32; k += kThreads) {
+    lds[L.bo + k] = k < a.A ? P[a.po.bo + k] : 0.0f;
+    lds[L.ls + k] = (a.po.ls >= 0 && k < a.A) ? P[a.po.ls + k] : 0.0f;
+  }
+}
+
+template <int AMAX, bool CONT>
+__global__ __launch_bounds__(kThreads, 4) void act_kernel(ActArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  load_weights_actor(lds_, a, tid);
+  __syncthreads();
+  const LdsLayout& L = a.L;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles;
+       tile += (int64_t)gridDim.x * kWaves) {
+    float* lds = opaque_base(lds_);
+    const int64_t i = tile * 32 + l31;
+    const bool valid = i < a.n;
+    const int64_t ic = valid ? i : 0;
+    f32x16 x[2], y[2];
+    x[0] = load_x0_obs(a.obs + ic * a.D, a.D, a.nq1, valid, h);
+    dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);       // y = h1
+    dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);                         // x = h2
+    dense_tanh(y, lds + L.Wa, lds + L.ba, x, l31, h);                         // y = actor hidden
+    float out[AMAX];
+    heads<AMAX>(out, lds + L.Wo, lds + L.bo, a.A, y, h);
+    if (!valid || h != 0) continue;
+    if (CONT) {
+      // Normal(mean, exp(log_std)).sample(): Box-Muller pairs from Philox (4 uniforms per call)
+      float* act = (float*)a.actions + i * a.A;
+#pragma unroll
+      for (int k0 = 0; k0 < AMAX; k0 += 4) {
+        if (k0 < a.A) {
+          uint32_t c[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32) ^ (uint32_t)(k0 << 24),
+                           a.ctr_lo, a.ctr_hi};
+          philox4x32(c, a.seed_lo, a.seed_hi);
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const float r = sqrtf(-2.0f * __logf(u01(c[2 * p])));
+            float sn, cs;
+            __sincosf(6.28318530717958647692f * u01(c[2 * p + 1]), &sn, &cs);
+            const int k = k0 + 2 * p;
+            if (k < a.A) act[k] = out[k] + __expf(lds[L.ls + k]) * (r * cs);
+            if (k + 1 < a.A) act[k + 1] = out[k + 1] + __expf(lds[L.ls + k + 1]) * (r * sn);
+          }
+        }
+      }
+    } else {
+      // Categorical(logits).sample() by inverse CDF on one uniform
+      uint32_t c[4] = {(uint32_t)i, (uint32_t)((uint64_t)i >> 32), a.ctr_lo, a.ctr_hi};
+      philox4x32(c, a.seed_lo, a.seed_hi);
+      float mx = out[0];
+#pragma unroll
+      for (int k = 1; k < AMAX; ++k)
+        if (k < a.A) mx = fmaxf(mx, out[k]);
+      float e[AMAX], se = 0.0f;
+#pragma unroll
+      for (int k = 0; k < AMAX; ++k) {
+        e[k] = k < a.A ? __expf(out[k] - mx) : 0.0f;
+        se += e[k];
+      }
+      // the first k whose cumulative mass exceeds u * sum (the last action takes the remainder)
+      const float target = u01(c[0]) * se;
+      int pick = a.A - 1;
+      float cum = 0.0f;
+#pragma unroll
+      for (int k = 0; k < AMAX; ++k) {
+        if (k < a.A - 1) {
+          cum += e[k];
+          if (pick == a.A - 1 && target < cum) pick = k;
+        }
+      }
+      ((int32_t*)a.actions)[i] = pick;
+    }
+  }
+}
+
 KArgs base_args(const MlpShape& sh, const ParamOffsets& po, const float* params) {
   KArgs k{};
   k.L = make_layout(sh);
@@ -376,6 +513,24 @@ void raise_lds_limits() {
   DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
   DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
 #undef DPPO_SET
+#define DPPO_SET(A, C)                                                                  \
+  (void)hipFuncSetAttribute((const void*)act_kernel<A, C>,                              \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
+  DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
+  DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
+#undef DPPO_SET
+}
+
+int cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
 }
 
 }  // namespace
@@ -412,6 +567,34 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
   int64_t g = (ntiles + kWaves - 1) / kWaves;
   if (g > 2 * cus) g = 2 * cus;
   DPPO_DISPATCH(eval_kernel, sh, dim3((unsigned)g), lds, s, k);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
+               void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s) {
+  if (n <= 0) return DPPO_OK;
+  ActArgs k{};
+  k.L = make_layout(sh);
+  k.po = po;
+  k.params = params;
+  k.obs = obs;
+  k.actions = actions;
+  k.n = n;
+  k.seed_lo = (uint32_t)seed;
+  k.seed_hi = (uint32_t)(seed >> 32);
+  k.ctr_lo = (uint32_t)counter;
+  k.ctr_hi = (uint32_t)(counter >> 32);
+  k.D = sh.D;
+  k.D8 = sh.D8;
+  k.nq1 = sh.D8 / 8;
+  k.A = sh.A;
+  const size_t lds = (size_t)k.L.total * sizeof(float);
+  raise_lds_limits();
+  const int64_t ntiles = (n + 31) / 32;
+  int64_t g = (ntiles + kWaves - 1) / kWaves;
+  if (g > 2 * cu_count()) g = 2 * cu_count();
+  DPPO_DISPATCH(act_kernel, sh, dim3((unsigned)g), lds, s, k);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

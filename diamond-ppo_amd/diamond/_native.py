@@ -28,7 +28,7 @@ EXPORTED = [
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_resolve",
+    "dppo_perm_targets_numpy", "dppo_perm_resolve", "dppo_act_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
                   "allreduce", "perm", "reduce_adam"]
@@ -94,6 +94,7 @@ def load():
         "dppo_adv_stats": (ctypes.c_int, [vp, vp, vp]),
         "dppo_adv_normalize_f32": (ctypes.c_int, [vp, vp, i64, vp]),
         "dppo_old_policy_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
+        "dppo_act_f32": (ctypes.c_int, [vp, vp, vp, i64, ctypes.c_uint64, ctypes.c_uint64, vp, vp]),
         "dppo_learn_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,
                                           P(LearnOutputs), vp]),
         "dppo_learn_targets_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,

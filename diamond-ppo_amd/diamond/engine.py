@@ -338,6 +338,37 @@ class NativeLearner:
             self.flat.flat.copy_(cpu)
 
     # -----------------------------------------------------------------------------------------
+    def act(self, observations: np.ndarray, seed: int) -> np.ndarray:
+        """Sample actions for a batch of observations with the fused actor kernel
+        (``dppo_act_f32``; default network only): pinned upload, one launch, pinned download.
+        Discrete actions come back int64 like the reference's ``Categorical.sample().numpy()``;
+        continuous ones float32 ``[n, A]``."""
+        if not self.fused:
+            raise RuntimeError("act() needs the default network (fused path)")
+        obs = np.asarray(observations, dtype=np.float32).reshape(-1, self.D)
+        n = obs.shape[0]
+        b = getattr(self, "_act_bufs", None)
+        if b is None or b["n"] != n:
+            dt = torch.float32 if self.continuous else torch.int32
+            shp = (n, self.A) if self.continuous else (n,)
+            b = {"n": n, "obs_h": torch.empty((n, self.D), dtype=torch.float32).pin_memory(),
+                 "obs_d": torch.empty((n, self.D), dtype=torch.float32, device=self.device),
+                 "act_d": torch.empty(shp, dtype=dt, device=self.device),
+                 "act_h": torch.empty(shp, dtype=dt).pin_memory(), "counter": 0}
+            self._act_bufs = b
+        b["obs_h"].numpy()[:] = obs
+        b["obs_d"].copy_(b["obs_h"], non_blocking=True)
+        s = torch.cuda.current_stream(self.device)
+        N.check(self.handle.lib.dppo_act_f32(self.handle.h, self.flat.flat.data_ptr(),
+                                             b["obs_d"].data_ptr(), n, seed & (2 ** 64 - 1),
+                                             b["counter"], b["act_d"].data_ptr(), s.cuda_stream),
+                "dppo_act_f32")
+        b["counter"] += 1
+        b["act_h"].copy_(b["act_d"], non_blocking=True)
+        s.synchronize()
+        out = b["act_h"].numpy()
+        return out.copy() if self.continuous else out.astype(np.int64)
+
     def _start_draft(self, key: np.ndarray, pos: int):
         """Draw the next learn's swap targets on a host thread (ctypes releases the GIL)."""
         slot = 1 - self._slot

@@ -108,6 +108,10 @@ class _AgentBase:
     default_network: type = None
     init_fn = staticmethod(network_parameter_init_)
     stage_rollout = True  # rollout() stages each step into HBM as the envs step (RolloutStager)
+    # rollout() samples the default network's actions with the fused actor kernel
+    # (dppo_act_f32: same distribution as get_actions, Philox draws instead of torch's); False, or
+    # any other network_cls, calls network.get_actions as the reference does
+    fused_actions = True
 
     def _setup(self, env_fn, cfg, network_cls, envs=None):
         self.device = require_gpu(getattr(cfg, "device_index", 0))
@@ -144,6 +148,8 @@ class _AgentBase:
         self.current_step = 0
         self._stager = None
         self._staged = None
+        base_seed = cfg.seed if cfg.seed is not None else torch.initial_seed()
+        self._act_seed = (int(base_seed) * 0x9E3779B97F4A7C15 + rank) & (2 ** 64 - 1)
 
     def _env_actions(self, actions: np.ndarray) -> np.ndarray:
         """What the environment receives for the sampled actions (identity; ContinuousPPO's
@@ -161,7 +167,10 @@ class _AgentBase:
         if stager is not None:
             stager.begin()
         for t in range(self.cfg.rollout_steps):
-            actions = self.network.get_actions(observations, device=self.device)
+            if self.fused_actions and self._learner.fused:
+                actions = self._learner.act(observations, self._act_seed)
+            else:
+                actions = self.network.get_actions(observations, device=self.device)
             next_observations, rewards, terminations, truncations, infos = self.envs.step(
                 self._env_actions(actions))
             experience.append([observations, next_observations, actions, rewards, terminations,

@@ -133,6 +133,15 @@ int dppo_old_policy_f32(dppo_handle* h, const float* params, const float* obs, c
                         const float* next_obs, float* log_probs, float* values, float* next_values,
                         int64_t n, void* stream);
 
+/* Rollout action sampling with the default actor MLP (replaces get_actions, ppo.py:73-82:
+ * Categorical(logits).sample(); continuous_ppo.py:83-93: Normal(mean, exp(log_std)).sample()).
+ * obs [n][D] on the device; actions out int32 [n] or float32 [n][A].  Randomness: Philox4x32-10
+ * keyed by `seed`, counter (sample index, `counter`) -- deterministic for a given
+ * (seed, counter), the same distribution as the reference's torch draws but not the same draws;
+ * advance `counter` once per call. */
+int dppo_act_f32(dppo_handle* h, const float* params, const float* obs, int64_t n, uint64_t seed,
+                 uint64_t counter, void* actions, void* stream);
+
 /* One full PPO.learn (ppo.py:224-287 / continuous_ppo.py:236-299) with the default network:
  * old-policy eval, GAE, returns, advantage normalisation, then num_epochs x num_minibatches
  * {gather, forward, clipped-surrogate + value + entropy loss, analytic backward, [RCCL

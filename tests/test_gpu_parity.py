@@ -423,3 +423,67 @@ def test_staged_rollout_learn_matches_unstaged(continuous):
         results.append(flat_params(agent))
     np.testing.assert_array_equal(results[0], results[1])
     np.testing.assert_array_equal(results[2], results[1])
+
+
+# ---------------------------------------------------------------------------------------------
+def _act_agent(continuous, D, A, Nn):
+    import gym_stub
+    np.random.seed(0)
+    torch.manual_seed(0)
+    envs = gym_stub.SyncVectorEnv(
+        [lambda: gym_stub.SyntheticEnv(D, A, continuous=continuous, act_dim=A)] * Nn)
+    Cfg = diamond.ContinuousPPOConfig if continuous else diamond.PPOConfig
+    Agent = diamond.ContinuousPPO if continuous else diamond.PPO
+    return Agent(None, Cfg(rollout_steps=8, num_envs=Nn, verbose=False), envs=envs)
+
+
+def test_fused_actions_categorical_distribution():
+    """dppo_act_f32 (rollout sampling, replaces get_actions ppo.py:73-82): deterministic per
+    (seed, counter), and its empirical action frequencies for one observation repeated 2^17 times
+    match the network's softmax probabilities within 5 sigma."""
+    D, A, n = 8, 4, 1 << 17
+    agent = _act_agent(False, D, A, 64)
+    with torch.no_grad():
+        agent.network.actor_out_layer.weight.mul_(100.0)   # spread the probabilities out
+    rng = np.random.default_rng(3)
+    o = rng.standard_normal(D).astype(np.float32)
+    obs = np.tile(o, (n, 1))
+    a1 = agent._learner.act(obs, 1234)
+    agent._learner._act_bufs["counter"] -= 1
+    a2 = agent._learner.act(obs, 1234)
+    a3 = agent._learner.act(obs, 1234)
+    assert a1.dtype == np.int64 and np.array_equal(a1, a2) and not np.array_equal(a2, a3)
+    with torch.no_grad():
+        logits, _ = agent.network.get_logits_and_values(torch.from_numpy(o).to(dev())[None])
+        p = torch.softmax(logits[0].double(), -1).cpu().numpy()
+    assert p.min() > 0.01 and p.max() < 0.97
+    freq = np.bincount(a1, minlength=A) / n
+    sig = np.sqrt(p * (1 - p) / n)
+    assert np.all(np.abs(freq - p) <= 5 * sig + 1e-12), (freq, p)
+    assert a1.min() >= 0 and a1.max() < A
+
+
+def test_fused_actions_gaussian_mean_and_scale():
+    """Continuous sampling: with log_std = -30 the samples ARE the actor means (checks the fused
+    forward against the torch module); with log_std = -0.5 the per-dimension sample mean and std
+    of 2^17 draws for one observation match mean / exp(log_std) within 5 sigma."""
+    D, A, n = 17, 6, 1 << 17
+    agent = _act_agent(True, D, A, 64)
+    rng = np.random.default_rng(4)
+    obs = rng.standard_normal((4096, D)).astype(np.float32)
+    with torch.no_grad():
+        agent.network.actor_log_std.fill_(-30.0)
+        mean, _, _ = agent.network.get_means_log_stds_and_values(torch.from_numpy(obs).to(dev()))
+    acts = agent._learner.act(obs, 99)
+    assert acts.dtype == np.float32 and acts.shape == (4096, A)
+    np.testing.assert_allclose(acts, mean.cpu().numpy(), rtol=0, atol=2e-5)
+    with torch.no_grad():
+        agent.network.actor_log_std.fill_(-0.5)
+    o = obs[:1]
+    with torch.no_grad():
+        mu = agent.network.get_means_log_stds_and_values(torch.from_numpy(o).to(dev()))[0][0]
+    mu = mu.cpu().numpy().astype(np.float64)
+    x = agent._learner.act(np.tile(o, (n, 1)), 7).astype(np.float64)
+    sd = np.exp(-0.5)
+    assert np.all(np.abs(x.mean(0) - mu) <= 5 * sd / np.sqrt(n))
+    assert np.all(np.abs(x.std(0) - sd) <= 5 * sd / np.sqrt(2 * n))
