@@ -127,8 +127,15 @@ def gae_roofline(device, T=128, N=8192, sets=16, reps=4):
     per = ms / cnt
     nbytes = 22 * T * N
     achieved = nbytes / (per * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(f"gae{N}", {}).get("gae")
+        except Exception:
+            traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "gae_pipe_kernel<32>", "num_envs": N, "rollout_steps": T,
             "bytes_per_launch": nbytes, "us_per_launch": round(per * 1e3, 2),
             "launches": cnt, "rotating_sets": sets}

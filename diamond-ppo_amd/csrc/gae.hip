@@ -140,9 +140,8 @@ __global__ __launch_bounds__(kThreads) void gae_kernel(
 
 // ---- Pipelined GAE (aligned shapes: the one learn() and the benchmark use) ---------------------
 // Persistent: at most one workgroup per CU, walking env tiles of E envs -- E = 32 (each row of a
-// [T][N] buffer one 128-B line) when that still gives every CU a tile, else E = 16 with blocks b
-// and b + 8 (one XCD under round-robin dispatch) taking the two halves of the same 128-B lines
-// (speed only).  The serial recurrence is the latency floor, so a workgroup scans ALL its envs in
+// [T][N] float buffer one 128-B line) when that still gives every CU a tile, else E = 16; tiles
+// that share 128-B lines run on one XCD (pipe_tile).  The serial recurrence is the latency floor, so a workgroup scans ALL its envs in
 // one pass: lanes are free, the 128 dependent steps are not.  9 waves per workgroup:
 //  * waves 0..7 each own one 16-step chunk of the current 128-step super-chunk (wave w chunk
 //    7 - w: waves issue roughly in wave order, so the chunk the scan needs first is requested
@@ -218,10 +217,16 @@ __device__ __forceinline__ void set_flag(int* f, int gen) {
   __hip_atomic_store(f, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// logical tile lb -> env tile: lb and lb + 8 (same XCD under round-robin) get 2p and 2p + 1
+// logical tile lb -> env tile, XCD-aware (speed only): the K = 128 / E tiles whose flag bytes
+// share one 128-B line of term / trunc (and, for E = 16, whose floats share lines pairwise) go to
+// blocks lb, lb + 8, lb + 16, ... -- one XCD under round-robin dispatch, so the line is fetched
+// into one L2 once instead of into K different XCDs' L2s (measured before: 4x the flag bytes,
+// 21 MB read per launch at N = 8192 for 14.7 MB of operands)
+template <int E>
 __device__ __forceinline__ int pipe_tile(int lb, int ntiles) {
-  const int grp = lb >> 4, r = lb & 15;
-  return (grp + 1) * 16 <= ntiles ? grp * 16 + 2 * (r & 7) + (r >> 3) : lb;
+  constexpr int K = 128 / E, G = 8 * K;
+  const int grp = lb / G, r = lb % G;
+  return (grp + 1) * G <= ntiles ? grp * G + K * (r & 7) + (r >> 3) : lb;
 }
 
 template <int E>
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     double lsum = 0.0, lsq = 0.0;
     int gen = 0;
     for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
-      const int n0 = (E == 16 ? pipe_tile(lb, ntiles) : lb) * E;
+      const int n0 = pipe_tile<E>(lb, ntiles) * E;
       for (int s = 0; s < nsup; ++s) {
         ++gen;
         const int hi = T - s * kPSuper;
@@ -453,45 +458,56 @@ __global__ void adv_normalize_kernel(float* __restrict__ adv, const float* __res
 
 // Sample records for the minibatch gather: rec[i] = obs[0..D8) (zero padded) |
 // {action bits, old log-prob, (normalised) advantage, return} | continuous actions (padded to 4).
-__global__ __launch_bounds__(256) void pack_kernel(PackArgs a) {
+// A block packs 256 consecutive samples through LDS: the [256][D] observation rows and the
+// [256][A] continuous actions are read as one contiguous run each, the [256][R] records are
+// assembled in LDS and leave as one contiguous run of 16-B stores (a record is R = 12..52 floats:
+// storing it per thread scattered 16-B pieces over every line and doubled the written bytes).
+constexpr int kPackTile = 256;
+
+__global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float pk_lds[];
+  float* obs_s = pk_lds;                          // [256][D]
+  float* act_s = obs_s + kPackTile * a.D;         // [256][A] (continuous)
+  float* rec_s = act_s + (a.continuous ? kPackTile * a.A : 0);  // [256][R], 16-B aligned rows
   float mean = 0.0f, denom = 1.0f;
   if (a.advantage_norm) {
     float sd;
     mean_std_from(a.dsum, a.n_total, &mean, &sd);
     denom = sd + 1e-6f;
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.B;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float* rec = a.rec + i * a.R;
-    const float* o = a.obs + i * a.D;
-    for (int k = 0; k < a.D8; k += 4) {
-      f32x4 w;
-      w[0] = k + 0 < a.D ? o[k + 0] : 0.0f;
-      w[1] = k + 1 < a.D ? o[k + 1] : 0.0f;
-      w[2] = k + 2 < a.D ? o[k + 2] : 0.0f;
-      w[3] = k + 3 < a.D ? o[k + 3] : 0.0f;
-      *(f32x4*)(rec + k) = w;
-    }
-    float adv = a.adv[i];
-    if (a.advantage_norm) adv = (adv - mean) / denom;  // ppo.py:243, fp32 as the reference
-    if (a.adv_out) a.adv_out[i] = adv;
-    f32x4 s;
-    s[0] = a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]);
-    s[1] = a.logp[i];
-    s[2] = adv;
-    s[3] = a.ret[i];
-    *(f32x4*)(rec + a.D8) = s;
+  const int t = threadIdx.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * kPackTile; i0 < a.B;
+       i0 += (int64_t)gridDim.x * kPackTile) {
+    const int ns = (int)min((int64_t)kPackTile, a.B - i0);
+    const float* o = a.obs + i0 * a.D;
+    for (int e = t; e < ns * a.D; e += kPackTile) obs_s[e] = o[e];
     if (a.continuous) {
-      const float* act = (const float*)a.actions + i * a.A;
-      for (int k = 0; k < a.A; k += 4) {
-        f32x4 w;
-        w[0] = k + 0 < a.A ? act[k + 0] : 0.0f;
-        w[1] = k + 1 < a.A ? act[k + 1] : 0.0f;
-        w[2] = k + 2 < a.A ? act[k + 2] : 0.0f;
-        w[3] = k + 3 < a.A ? act[k + 3] : 0.0f;
-        *(f32x4*)(rec + a.D8 + 4 + k) = w;
+      const float* ac = (const float*)a.actions + i0 * a.A;
+      for (int e = t; e < ns * a.A; e += kPackTile) act_s[e] = ac[e];
+    }
+    __syncthreads();
+    if (t < ns) {
+      const int64_t i = i0 + t;
+      float* r = rec_s + t * a.R;
+      for (int k = 0; k < a.D8; ++k) r[k] = k < a.D ? obs_s[t * a.D + k] : 0.0f;
+      float adv = a.adv[i];
+      if (a.advantage_norm) adv = (adv - mean) / denom;  // ppo.py:243, fp32 as the reference
+      if (a.adv_out) a.adv_out[i] = adv;
+      r[a.D8 + 0] = a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]);
+      r[a.D8 + 1] = a.logp[i];
+      r[a.D8 + 2] = adv;
+      r[a.D8 + 3] = a.ret[i];
+      if (a.continuous) {
+        const int na = a.R - a.D8 - 4;
+        for (int k = 0; k < na; ++k) r[a.D8 + 4 + k] = k < a.A ? act_s[t * a.A + k] : 0.0f;
       }
     }
+    __syncthreads();
+    // the tile's records are contiguous in memory: ns * R floats, R a multiple of 4
+    f32x4* dst = (f32x4*)(a.rec + i0 * a.R);
+    const f32x4* src = (const f32x4*)rec_s;
+    for (int c = t; c < ns * a.R / 4; c += kPackTile) dst[c] = src[c];
+    __syncthreads();
   }
 }
 
@@ -581,7 +597,14 @@ int launch_adv_normalize(float* adv, const float* mean_std, int64_t n, hipStream
 
 int launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.B <= 0) return DPPO_OK;
-  DPPO_LAUNCH(pack_kernel, dim3(grid_for(a.B, 256)), dim3(256), 0, s, a);
+  const size_t lds = (size_t)kPackTile * (a.D + (a.continuous ? a.A : 0) + a.R) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {  // up to 100 KB at D = 32, A = 16
+    attr = true;
+    (void)hipFuncSetAttribute((const void*)pack_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  }
+  DPPO_LAUNCH(pack_kernel, dim3(grid_for(a.B, kPackTile)), dim3(kPackTile), lds, s, a);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

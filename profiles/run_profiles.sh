@@ -26,3 +26,14 @@ echo "pmc3 done"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc4 \
   -o p4 -- python3 $B --steps 2 --warmup 1 > $OUT/pmc4.log 2>&1
 echo "pmc4 done"
+# GAE at N = 8192 (bench.py roofline_gae): 16 rotating 23 MB buffer sets
+G="$R/tools/gae_bench.py --N 8192"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/gkt -o gkt -- \
+  python3 $G --reps 4 > $OUT/gkt.log 2>&1
+echo "gae kernel trace done"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/gpmc3 -o g3 -- \
+  python3 $G --reps 1 > $OUT/gpmc3.log 2>&1
+echo "gae pmc3 done"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/gpmc4 \
+  -o g4 -- python3 $G --reps 1 > $OUT/gpmc4.log 2>&1
+echo "gae pmc4 done"

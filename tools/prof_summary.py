@@ -148,6 +148,37 @@ def main():
             if ln.startswith("{"):
                 lines += ["", "## bench.py line of the kernel-trace run", "", "```", ln.strip(),
                           "```"]
+    # GAE at N = 8192 (bench.py roofline_gae), from the gae_bench.py passes
+    gstats = os.path.join(P, "gkt", "gkt_kernel_stats.csv")
+    if os.path.exists(gstats):
+        shutil.copy(gstats, os.path.join(out_dir, f"{a.tag}_gae8192_kernel_stats.csv"))
+        lines += ["", "## GAE at num_envs = 8192 (tools/gae_bench.py, 16 rotating 23 MB sets)", "",
+                  "| kernel | calls | avg µs | min µs | max µs |", "|---|---|---|---|---|"]
+        for r in csv.DictReader(open(gstats)):
+            if base(r["Name"]) in ("gae_pipe_kernel", "gae_kernel"):
+                lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | "
+                             f"{float(r['AverageNs']) / 1e3:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
+                             f"{float(r['MaxNs']) / 1e3:.2f} |")
+        g = {}
+        for k in ("gpmc3/g3", "gpmc4/g4"):
+            f = os.path.join(P, k + "_counter_collection.csv")
+            if os.path.exists(f):
+                for kern, d in load_pmc(f).items():
+                    if base(kern) == "gae_pipe_kernel":
+                        g.update(d)
+        if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
+            rd, wr = 2 * g["FETCH_SIZE"] * 1024, g["WRITE_SIZE"] * 1024
+            lines += ["", f"HBM traffic per launch: read {rd / 1e6:.2f} MB (2 x FETCH_SIZE), write "
+                      f"{wr / 1e6:.2f} MB (algorithmic: 14 B + 8 B per element = 14.68 + 8.39 MB)"]
+            pj = os.path.join(out_dir, "pmc_traffic.json")
+            allt = json.load(open(pj)) if os.path.exists(pj) else {}
+            allt["gae8192"] = {"gae": int(rd + wr)}
+            json.dump(allt, open(pj, "w"), indent=1, sort_keys=True)
+        glog = os.path.join(P, "gkt.log")
+        if os.path.exists(glog):
+            for ln in open(glog):
+                if ln.startswith("{"):
+                    lines += ["", "```", ln.strip(), "```"]
     open(os.path.join(out_dir, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
