@@ -92,6 +92,8 @@ struct Lds2 {  // offsets (floats)
   int Wv;                  // [64] permuted
   int b1, b2, ba, bc;      // [64] natural order
   int bo, ls, bv;          // [16] [16] [4]
+  int gc;                  // [4][16] Gaussian per-action constants (continuous), see prologue
+  int gent;                // [4] {sum over actions of the Gaussian entropy terms}
   int X0[2], H1[2], H2[2], DZAC[2];  // team 0 -> team 1 hand-off, double-buffered by step parity
   int HAC, DOUT;           // team 0 only: [ha | hc] activations, per-sample head deltas
   int DZ2, DZ1;            // team 1 only
@@ -131,6 +133,8 @@ Lds2 make_lds2(int D16) {
   L.bo = take(16);
   L.ls = take(16);
   L.bv = take(4);
+  L.gc = take(4 * 16);
+  L.gent = take(4);
   L.SX0 = D16 + 4;
   for (int b = 0; b < 2; ++b) {
     L.X0[b] = take(S * L.SX0);
@@ -356,6 +360,28 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     lds_[L.ls + k] = (po.ls >= 0 && k < a.A) ? P[po.ls + k] : 0.0f;
   }
   if (tid < 4) lds_[L.bv + tid] = tid == 0 ? P[po.bv] : 0.0f;
+  if (CONT && tid < 16) {
+    // Normal(mean, exp(log_std)) constants of action k, the same for every sample: computed once
+    // per minibatch instead of an exp, a log and IEEE divisions per sample and action
+    // (continuous_ppo.py:41-47; torch Normal.log_prob / entropy)
+    const bool on = po.ls >= 0 && tid < a.A;
+    const float sg = on ? __expf(P[po.ls + tid]) : 1.0f;
+    const float lsc = on ? __logf(sg) : 0.0f;
+    lds_[L.gc + tid] = on ? 1.0f / (2.0f * (sg * sg)) : 0.0f;  // 1 / (2 var), 0 past A
+    lds_[L.gc + 16 + tid] = 1.0f / (sg * sg);       // 1 / var
+    lds_[L.gc + 32 + tid] = 1.0f / sg;              // 1 / sigma
+    lds_[L.gc + 48 + tid] = lsc;                    // log sigma
+    if (tid == 0) {
+      float e = 0.0f, c = 0.0f;
+      for (int k = 0; k < a.A && k < 16; ++k) {
+        const float l = __logf(__expf(P[po.ls + k]));
+        e += kHalfLog2PiPlusHalf + l;  // entropy (continuous_ppo.py:45-47)
+        c += l + kLogSqrt2Pi;          // log-prob constant part
+      }
+      lds_[L.gent] = e;
+      lds_[L.gent + 1] = c;
+    }
+  }
 
   if (team == 0) {
     // =========================== forward team ===========================
@@ -506,23 +532,20 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         const f32x4 ha0 = *(const f32x4*)(hrow + 4 * hj), ha1 = *(const f32x4*)(hrow + 32 + 4 * hj);
         const f32x4 hc0 = *(const f32x4*)(hrow + 64 + 4 * hj);
         const f32x4 hc1 = *(const f32x4*)(hrow + 96 + 4 * hj);
+        // all AMAX rows, branch-free (head-image rows and biases k >= A are zero, so out[k] = 0):
+        // the AMAX independent dot / DPP chains interleave instead of running one by one
         float out[AMAX];
 #pragma unroll
         for (int k = 0; k < AMAX; ++k) {
-          float part = 0.f;
-          if (k < a.A) {
-            f32x4 w0, w1;
-            if (WREG) {
-              w0 = (f32x4){woh[k][0], woh[k][1], woh[k][2], woh[k][3]};
-              w1 = (f32x4){woh[k][4], woh[k][5], woh[k][6], woh[k][7]};
-            } else {
-              w0 = *(const f32x4*)(lds + L.Wo + k * H + 4 * hj);
-              w1 = *(const f32x4*)(lds + L.Wo + k * H + 32 + 4 * hj);
-            }
-            part = dot8(w0, w1, ha0, ha1);
+          f32x4 w0, w1;
+          if (WREG) {
+            w0 = (f32x4){woh[k][0], woh[k][1], woh[k][2], woh[k][3]};
+            w1 = (f32x4){woh[k][4], woh[k][5], woh[k][6], woh[k][7]};
+          } else {
+            w0 = *(const f32x4*)(lds + L.Wo + k * H + 4 * hj);
+            w1 = *(const f32x4*)(lds + L.Wo + k * H + 32 + 4 * hj);
           }
-          part = sum8(part);
-          out[k] = part + lds[L.bo + k];
+          out[k] = sum8(dot8(w0, w1, ha0, ha1)) + lds[L.bo + k];
         }
         float vp = 0.f;
         {
@@ -541,21 +564,19 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         HEAD_STAMP(0);
         const float adv = sc[2], ret = sc[3];
         float logp = 0.f, ent = 0.f;
-        float p[AMAX], lp[AMAX], xa[AMAX], sig[AMAX];
+        float p[AMAX], lp[AMAX], xa[AMAX];
         if (CONT) {
+          // sum_k [-(x-mu)^2 / (2 var) - log sigma - log sqrt(2 pi)] as
+          // -sum_k (x-mu)^2 / (2 var) - sum_k (log sigma + log sqrt(2 pi)); 1/(2 var) is 0 for k >= A
+          float q = 0.f;
 #pragma unroll
           for (int k = 0; k < AMAX; ++k) {
-            xa[k] = 0.f;
-            sig[k] = 1.f;
-            if (k < a.A) {
-              xa[k] = cact[k >> 2][k & 3];
-              sig[k] = __expf(lds[L.ls + k]);
-              const float lsc = __logf(sig[k]);
-              const float d = xa[k] - out[k];
-              logp += -(d * d) / (2.0f * (sig[k] * sig[k])) - lsc - kLogSqrt2Pi;
-              ent += kHalfLog2PiPlusHalf + lsc;
-            }
+            xa[k] = cact[k >> 2][k & 3];  // zero past A (record padding / unloaded chunks)
+            const float d = xa[k] - out[k];
+            q += (d * d) * lds[L.gc + k];
           }
+          logp = -q - lds[L.gent + 1];
+          ent = lds[L.gent];
         } else {
           const int actn = __float_as_int(sc[0]);
           float mx = out[0];
@@ -570,14 +591,10 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
           const float lse = mx + __builtin_amdgcn_logf(se) * kLn2;
 #pragma unroll
           for (int k = 0; k < AMAX; ++k) {
-            lp[k] = 0.f;
-            p[k] = 0.f;
-            if (k < a.A) {
-              lp[k] = out[k] - lse;
-              p[k] = __expf(lp[k]);
-              ent -= p[k] * lp[k];
-              if (k == actn) logp = lp[k];
-            }
+            lp[k] = out[k] - lse;
+            p[k] = k < a.A ? __expf(lp[k]) : 0.f;  // p = 0 past A: no head delta, no entropy
+            ent -= p[k] * lp[k];
+            logp = k == actn ? lp[k] : logp;
           }
         }
         HEAD_STAMP(1);
@@ -599,12 +616,12 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         float* drow = DOUT + hs * SD;
 #pragma unroll
         for (int k = 0; k < AMAX; ++k) {
-          if (k < a.A && (k & 7) == hj) {
+          if ((k & 7) == hj) {  // k >= A: zero deltas / log-std slots nobody reads
             float dk, dl = 0.f;
             if (CONT) {
               const float dd = xa[k] - out[k];
-              const float z = dd / sig[k];
-              dk = dlogp * dd / (sig[k] * sig[k]);
+              const float z = dd * lds[L.gc + 32 + k];
+              dk = dlogp * dd * lds[L.gc + 16 + k];
               dl = dlogp * (z * z - 1.0f);
             } else {
               const int actn = __float_as_int(sc[0]);
@@ -638,7 +655,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
             const f32x4 dk = *(const f32x4*)(drow + 4 * c);  // broadcast read
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (4 * c + e < a.A) gWo[4 * c + e] += dk[e] * ha;
+              if (4 * c + e < AMAX) gWo[4 * c + e] += dk[e] * ha;  // rows >= A: zero deltas
           }
           gWv += drow[32] * hc;
           gbh += drow[lane];  // lanes < A: bo; lane 32: bv; lanes 33..: log-std terms
@@ -659,8 +676,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
             float acc = 0.f;
 #pragma unroll
             for (int k = 0; k < AMAX; ++k)
-              if (k < a.A) acc += (WREG ? wod[k < AR ? k : 0][r] : lds[L.Wo + k * H + col]) *
-                                  dk[k >> 2][k & 3];
+              acc += (WREG ? wod[k < AR ? k : 0][r] : lds[L.Wo + k * H + col]) *
+                     dk[k >> 2][k & 3];  // head-image rows >= A are zero
             const float y = har[sb][r];
             dza[sb][r] = acc * (1.0f - y * y);
             const float yc = hcr[sb][r];

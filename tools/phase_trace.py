@@ -30,11 +30,15 @@ NI = len(NAMES0)  # barriers per interval set
 
 
 def main():
-    T, Nn, D, A = 128, int(os.environ.get("ABL_N", "4096")), 4, 2
-    cfg = diamond.PPOConfig(rollout_steps=T, num_envs=Nn, verbose=False)
-    agent = diamond.PPO(None, cfg, envs=bench.SpecEnvs(D, A, False))
+    # PHASE_CONFIG: a bench.py config name (default cartpole4096)
+    _, T, Nn, D, A, cont, pt, ptr = bench.CONFIGS[os.environ.get("PHASE_CONFIG", "cartpole4096")]
+    Nn = int(os.environ.get("ABL_N", Nn))
+    Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
+    Agent = diamond.ContinuousPPO if cont else diamond.PPO
+    cfg = Cfg(rollout_steps=T, num_envs=Nn, verbose=False)
+    agent = Agent(None, cfg, envs=bench.SpecEnvs(D, A, cont))
     dev = agent.device
-    ro, _ = bench.synth_rollout(T, Nn, D, A, False, 0.02, 0.005, 0, dev)
+    ro, _ = bench.synth_rollout(T, Nn, D, A, cont, pt, ptr, 0, dev)
     agent.learn_device(ro)
     torch.cuda.synchronize()
     L = agent._learner
