@@ -141,8 +141,9 @@ __global__ __launch_bounds__(kThreads) void gae_kernel(
 // ---- Pipelined GAE (aligned shapes: the one learn() and the benchmark use) ---------------------
 // Persistent: at most one workgroup per CU, walking env tiles of E envs -- E = 32 (each row of a
 // [T][N] float buffer one 128-B line) when that still gives every CU a tile, else E = 16; tiles
-// that share 128-B lines run on one XCD (pipe_tile).  The serial recurrence is the latency floor, so a workgroup scans ALL its envs in
-// one pass: lanes are free, the 128 dependent steps are not.  9 waves per workgroup:
+// that share 128-B lines run on one XCD (pipe_tile).  The serial recurrence is the latency floor,
+// so a workgroup scans ALL its envs in one pass: lanes are free, the 128 dependent steps are not.
+// 9 waves per workgroup:
 //  * waves 0..7 each own one 16-step chunk of the current 128-step super-chunk (wave w chunk
 //    7 - w: waves issue roughly in wave order, so the chunk the scan needs first is requested
 //    first; measured 0.4-0.6 us better than wave w -> chunk w at N = 8192).  An owner loads
@@ -213,8 +214,18 @@ __device__ __forceinline__ void wait_flag(int* f, int gen) {
     __builtin_amdgcn_s_sleep(1);
 }
 
+// Publish LDS data to the other waves of the workgroup: a wave's LDS operations are performed in
+// program order, so a flag store issued after the data stores is seen after them by any wave that
+// reads the flag and then the data -- no s_waitcnt lgkmcnt(0) (what a release would emit) in
+// front of it; only the compiler must keep the order (signal fence).  DPPO_GAE_RELEASE: the
+// release store (A/B timing).
 __device__ __forceinline__ void set_flag(int* f, int gen) {
+#ifdef DPPO_GAE_RELEASE
   __hip_atomic_store(f, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __hip_atomic_store(f, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
 }
 
 // logical tile lb -> env tile, XCD-aware (speed only): the K = 128 / E tiles whose flag bytes
