@@ -56,6 +56,22 @@ constexpr int kWave = 64;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// tanh of two activations: t = e^{-2|x|} = 2^{|x| (-2 log2 e)} (the same bits as __expf(-2|x|):
+// scaling by 2 commutes with the rounding), tanh = sign(x) (1 - t) / (1 + t) with one hardware
+// reciprocal; the non-transcendental steps run as packed-f32 ops on the pair (v_pk_mul/add_f32).
+// Absolute error <= ~1.5e-7 (1 - t cancels near 0: relative, not absolute, accuracy is lost).
+__device__ __forceinline__ f32x2 tanh2(f32x2 x) {
+  constexpr float kM2Log2e = -2.0f * 1.44269504088896340736f;
+  const f32x2 ax = {__builtin_fabsf(x[0]), __builtin_fabsf(x[1])};
+  const f32x2 y = ax * kM2Log2e;
+  const f32x2 t = {__builtin_amdgcn_exp2f(y[0]), __builtin_amdgcn_exp2f(y[1])};
+  const f32x2 d = t + 1.0f;
+  const f32x2 r = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  const f32x2 q = (1.0f - t) * r;
+  return {__builtin_copysignf(q[0], x[0]), __builtin_copysignf(q[1], x[1])};
+}
 
 // Launchers implemented in the .hip files (all stream-ordered, no host sync).
 int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,

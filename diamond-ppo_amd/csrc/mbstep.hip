@@ -288,7 +288,16 @@ __device__ __forceinline__ void tanh_rows(f32x4 (&v)[NSB]) {
 #pragma unroll
   for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[sb][r] = tanh_f(v[sb][r]);
+    for (int r = 0; r < 4; r += 2) {
+#ifdef DPPO_ABL_NOTANH
+      v[sb][r] *= 0.5f;
+      v[sb][r + 1] *= 0.5f;
+#else
+      const f32x2 y = tanh2((f32x2){v[sb][r], v[sb][r + 1]});
+      v[sb][r] = y[0];
+      v[sb][r + 1] = y[1];
+#endif
+    }
 }
 
 // dW rows (16q..) += sum over the S staged samples: A = dZ image (cols perm(o)), B = X image

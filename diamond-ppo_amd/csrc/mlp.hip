@@ -146,7 +146,11 @@ __device__ __forceinline__ float tanh_f(float x) {
 
 __device__ __forceinline__ void tanh_inplace(f32x16& x) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) x[r] = tanh_f(x[r]);
+  for (int r = 0; r < 16; r += 2) {
+    const f32x2 y = tanh2((f32x2){x[r], x[r + 1]});
+    x[r] = y[0];
+    x[r + 1] = y[1];
+  }
 }
 
 // out = tanh(W X + b), W: [64][64] LDS image (stride SW), X: 2 k-blocks.
