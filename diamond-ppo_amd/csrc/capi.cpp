@@ -462,8 +462,13 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
           DPPO_TRY(launch_mb(h->sh, h->po, ga, G, s));
         }
         Timed tm(h, K_RADAM, s);
+#ifdef DPPO_ABL_RADAM_G1
+        const int Gr = 1;  // timing-only ablation: the fixed cost of the launch without slab reads
+#else
+        const int Gr = G;
+#endif
         DPPO_TRY(launch_reduce_adam(
-            h->slabs, G, h->slab_stride, h->layout.total, h->grad, h->sq_part, h->po.ls,
+            h->slabs, Gr, h->slab_stride, h->layout.total, h->grad, h->sq_part, h->po.ls,
             d.continuous ? d.act_dim : 0, hp->entropy_beta, d.continuous ? 1 : 0, h->arrivals,
             ++h->radam_epoch, params, adam_m, adam_v, hp->grad_norm_clip, (float)(-step_size), (float)bc2_sqrt,
             hp->adam_beta1, hp->adam_beta2, hp->adam_eps, trace, inv_m, hp->value_loss_weight,
@@ -561,7 +566,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
-  chk(dalloc(&h->arrivals, 16));
+  chk(dalloc(&h->arrivals, kArrivalWords));
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->B));
     chk(dalloc(&h->targets_dev2[k], E * h->B));
@@ -592,7 +597,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   if (rc == DPPO_OK) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
-    (void)hipMemset(h->arrivals, 0, 16 * sizeof(unsigned));
+    (void)hipMemset(h->arrivals, 0, kArrivalWords * sizeof(unsigned));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }

@@ -97,6 +97,10 @@ struct PackArgs {
 };
 int launch_pack(const PackArgs& a, hipStream_t s);
 
+// reduce_adam_kernel's arrival words: [0] top counter, [32 (1 + x)] the counter of XCD group x
+// (blockIdx % 8), [32 * 9] the release word; each on its own 128-B line
+constexpr int kArrivalWords = 32 * 10;
+
 // Default actor-critic MLP (hidden 64) kernels: mlp.hip.
 struct MlpShape {
   int D, D8, A, continuous, R;  // R = record stride (floats)

@@ -210,9 +210,31 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+#ifdef DPPO_ABL_ONECOUNTER
     __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned* wait_word = arrivals;
     const unsigned target = epoch * gridDim.x;
-    for (int spins = 0; (int)(__hip_atomic_load(arrivals, __ATOMIC_RELAXED,
+#else
+    // Fan-in sharded by XCD group (blockIdx % 8, one XCD under round-robin dispatch; any
+    // placement is correct): ~G/8 arrivals per counter instead of G serialised atomics on one
+    // word (~13 ns each, MI355X_MICROARCH.md fanin), the last arriver of each group adds to the
+    // top counter, the last of those publishes the release word -- which the waiters poll, so
+    // their loads never queue in front of the arrival atomics.
+    const unsigned x = blockIdx.x & 7;
+    const unsigned nx = (gridDim.x - x + 7) / 8;
+    const unsigned ng = gridDim.x < 8 ? gridDim.x : 8;
+    unsigned* wait_word = arrivals + 32 * 9;
+    const unsigned target = epoch;
+    const unsigned o1 = __hip_atomic_fetch_add(arrivals + 32 * (1 + x), 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    if (o1 == epoch * nx - 1) {
+      const unsigned o2 = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if (o2 == epoch * ng - 1)
+        __hip_atomic_store(wait_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+    for (int spins = 0; (int)(__hip_atomic_load(wait_word, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
          ++spins) {
       if (spins > (1 << 22)) break;  // never expected: the grid is resident
