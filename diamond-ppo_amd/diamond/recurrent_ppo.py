@@ -173,11 +173,14 @@ class RecurrentPPO:
         dev = self.device
         f = lambda x: torch.as_tensor(x, device=dev).to(torch.float32).contiguous()
         u8 = lambda x: (torch.as_tensor(x, device=dev) != 0).to(torch.uint8).contiguous()
+        # every operand bound to a name until the launch is enqueued: a temporary's block would go
+        # back to the caching allocator at once and could be handed to the next operand's copy
         r, v, nv = f(rewards), f(values), f(next_values)
+        te, tr = u8(terminations), u8(truncations)
         adv, ret = torch.empty_like(r), torch.empty_like(r)
         stream = torch.cuda.current_stream(dev).cuda_stream
         N.check(self.handle.lib.dppo_gae_f32(
-            self.handle.h, r.data_ptr(), u8(terminations).data_ptr(), u8(truncations).data_ptr(),
+            self.handle.h, r.data_ptr(), te.data_ptr(), tr.data_ptr(),
             v.data_ptr(), nv.data_ptr(), adv.data_ptr(), ret.data_ptr(), float(self.cfg.gamma),
             float(self.cfg.gae_lambda), stream), "dppo_gae_f32")
         return adv

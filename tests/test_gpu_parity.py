@@ -487,3 +487,104 @@ def test_fused_actions_gaussian_mean_and_scale():
     sd = np.exp(-0.5)
     assert np.all(np.abs(x.mean(0) - mu) <= 5 * sd / np.sqrt(n))
     assert np.all(np.abs(x.std(0) - sd) <= 5 * sd / np.sqrt(2 * n))
+
+
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["cartpole_small", "cheetah_small"])
+def test_generic_network_path_matches_reference_trace(name):
+    """A custom network_cls (here a subclass of the default network, which the fused kernels do
+    not claim) takes the generic path: the module under torch autograd on the GPU, GAE /
+    normalisation / clip + Adam in the HIP kernels.  It must reproduce the reference's captured
+    learn() like the fused path does."""
+    z = load_golden(f"learn_{name}.npz")
+    T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
+    base = diamond.continuous_ppo.ContinuousActorCriticNetwork if cont else \
+        diamond.ppo.ActorCriticNetwork
+
+    class CustomNet(base):
+        pass
+
+    import gym_stub
+    Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
+    Agent = diamond.ContinuousPPO if cont else diamond.PPO
+    kw = {k: z["cfg/" + k].item() for k in ("num_epochs", "num_minibatches", "lr", "adam_eps",
+                                             "gamma", "gae_lambda", "ppo_clip",
+                                             "value_loss_weight", "entropy_beta",
+                                             "grad_norm_clip", "total_steps")}
+    cfg = Cfg(rollout_steps=T, num_envs=Nn, verbose=False,
+              advantage_norm=bool(z["cfg/advantage_norm"]), decay_lr=bool(z["cfg/decay_lr"]), **kw)
+    envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(D, A, continuous=bool(cont),
+                                                                 act_dim=A)] * Nn)
+    agent = Agent(None, cfg, network_cls=CustomNet, envs=envs)
+    assert not agent._learner.fused
+    sd = {n: torch.from_numpy(z["init/" + n]) for n in z["param_names"]}
+    if hasattr(agent.network, "actor_out_layer"):
+        sd["actor_out_layer.weight"] = sd["actor_head.2.weight"]
+        sd["actor_out_layer.bias"] = sd["actor_head.2.bias"]
+    agent.network.load_state_dict(sd)
+    for li in range(n_learn):
+        np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
+                             int(z[f"rng_pos_before{li}"]), 0, 0.0))
+        agent.learn(experience(z, li))
+        torch.cuda.synchronize()
+    for n, p in agent.network.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), z["final/" + n], rtol=0, atol=5e-6,
+                                   err_msg=n)
+
+
+def test_checkpoint_roundtrip_continues_identically():
+    """Checkpointer (utils.py:584-619 format) save -> load_checkpoint into a fresh agent -> the
+    next learn() gives bit-identical parameters and Adam moments to the uninterrupted agent."""
+    import tempfile
+    z = load_golden("learn_lunar_medium.npz")
+    a1 = make_agent(z)
+    np.random.seed(3)
+    a1.learn(experience(z, 0))
+    torch.cuda.synchronize()
+    with tempfile.TemporaryDirectory() as d:
+        a1.checkpointer.folder = __import__("pathlib").Path(d)
+        a1.checkpointer.save(1, a1.network, a1.optimizer)
+        path = sorted(__import__("pathlib").Path(d).glob("*.pt"))[0]
+        a2 = make_agent(z)
+        a2.load_checkpoint(path)
+    st = np.random.get_state()
+    a1.learn(experience(z, 0))
+    np.random.set_state(st)
+    a2.learn(experience(z, 0))
+    torch.cuda.synchronize()
+    assert np.array_equal(flat_params(a1), flat_params(a2))
+    for p1, p2 in zip(a1.network.parameters(), a2.network.parameters()):
+        s1, s2 = a1.optimizer.state[p1], a2.optimizer.state[p2]
+        assert torch.equal(s1["exp_avg"], s2["exp_avg"])
+        assert torch.equal(s1["exp_avg_sq"], s2["exp_avg_sq"])
+        assert float(s1["step"]) == float(s2["step"])
+
+
+def test_recurrent_ppo_rollout_and_learn_run():
+    """RecurrentPPO (the reference's crashes at recurrent_ppo.py:78; intended semantics here):
+    train() -- rollout() and learn() -- runs on the stub env, changes the parameters, keeps them
+    finite, and its calculate_advantage is the bit-exact GAE kernel."""
+    import gym_stub
+    from oracle import ppo_np as P
+    np.random.seed(0)
+    torch.manual_seed(0)
+    T, Nn, D, A = 16, 8, 4, 2
+    envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(D, A)] * Nn)
+    cfg = diamond.RecurrentPPOConfig(rollout_steps=T, num_envs=Nn, verbose=False, num_epochs=2,
+                                     total_steps=2 * T * Nn)
+    agent = diamond.RecurrentPPO(None, cfg, envs=envs)
+    before = flat_params(agent)
+    agent.train()  # two rollout() + learn() iterations
+    torch.cuda.synchronize()
+    after = flat_params(agent)
+    assert np.all(np.isfinite(after)) and not np.array_equal(before, after)
+    rng = np.random.default_rng(2)
+    r = rng.normal(1, 1, (T, Nn)).astype(np.float32)
+    te = (rng.random((T, Nn)) < 0.1).astype(np.float32)
+    tr = (rng.random((T, Nn)) < 0.05).astype(np.float32)
+    v = rng.standard_normal((T, Nn)).astype(np.float32)
+    nv = rng.standard_normal((T, Nn)).astype(np.float32)
+    adv = agent.calculate_advantage(torch.from_numpy(r), torch.from_numpy(te),
+                                    torch.from_numpy(tr), torch.from_numpy(v),
+                                    torch.from_numpy(nv))
+    assert np.array_equal(adv.cpu().numpy(), P.gae(r, te, tr, v, nv))
