@@ -94,6 +94,7 @@ struct Lds2 {  // offsets (floats)
   int bo, ls, bv;          // [16] [16] [4]
   int gc;                  // [4][16] Gaussian per-action constants (continuous), see prologue
   int gent;                // [4] {sum over actions of the Gaussian entropy terms}
+  int PART;                // [4][S][16] per-wave partial head outputs (MFMA heads, AMAX == 8)
   int X0[2], H1[2], H2[2], DZAC[2];  // team 0 -> team 1 hand-off, double-buffered by step parity
   int HAC, DOUT;           // team 0 only: [ha | hc] activations, per-sample head deltas
   int DZ2, DZ1;            // team 1 only
@@ -143,6 +144,7 @@ Lds2 make_lds2(int D16) {
     L.DZAC[b] = take(S * SAC);
   }
   L.HAC = take(S * SAC);
+  L.PART = take(kTeamWaves * S * 16);
   L.DOUT = take(S * SD);
   L.DZ2 = take(S * SA);
   L.DZ1 = take(S * SA);
@@ -478,6 +480,27 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         wvd[j] = lds_[L.Wv + row0 + 4 * j + h4];
       }
     }
+    // MFMA heads (AMAX == 8, up to 8 actions): the head outputs are [16 rows = A logits / means,
+    // row 8 = value] x samples.  Each wave multiplies the 16 head-input features it owns (its rows
+    // of ha and hc, already in registers after interval 3) -- 8 v_mfma_f32_16x16x4_f32 per sample
+    // tile, A = its Wo / Wv columns, B = its activation registers -- and leaves the partial in
+    // LDS; the heads phase sums the four partials instead of 8-lane dot products + DPP trees.
+    // The head back-propagation dZa = Wo^T dout is two MFMA k-steps on the same layout.
+    constexpr bool MH = AMAX == 8;
+    float woA[MH ? 4 : 1], wvA[MH ? 4 : 1], woT[MH ? 2 : 1];
+    if (MH) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = row0 + 4 * h4 + r;
+        woA[r] = l15 < a.A ? P[po.Wo + l15 * H + f] : 0.0f;
+        wvA[r] = l15 == AMAX ? P[po.Wv + f] : 0.0f;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int k = 4 * t + h4;
+        woT[t] = k < a.A ? P[po.Wo + k * H + row0 + l15] : 0.0f;
+      }
+    }
 #ifdef DPPO_PHASE_TRACE
     int tr_k_ = 0;
 #endif
@@ -527,6 +550,19 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         tanh_rows(hcr);
         put_rows(HAC, SAC, row0, har, l15, h4);
         put_rows(HAC, SAC, 64 + row0, hcr, l15, h4);
+        if (MH) {
+          float* part = lds + L.PART + q * S * 16;
+#pragma unroll
+          for (int sb = 0; sb < NSB; ++sb) {
+            f32x4 o = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o = mfma16(woA[r], har[sb][r], o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o = mfma16(wvA[r], hcr[sb][r], o);
+            // lane (sample 16 sb + l15, h4) holds head rows 4 h4 .. 4 h4 + 3
+            *(f32x4*)(part + (16 * sb + l15) * 16 + 4 * h4) = o;
+          }
+        }
       }
       STEP_BARRIER();
       // ---- (4) heads + loss (VALU, 8 lanes per sample)
@@ -544,6 +580,21 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         // all AMAX rows, branch-free (head-image rows and biases k >= A are zero, so out[k] = 0):
         // the AMAX independent dot / DPP chains interleave instead of running one by one
         float out[AMAX];
+        float vmh = 0.f;
+        if (MH) {
+          f32x4 s0 = (f32x4){0.f, 0.f, 0.f, 0.f}, s1 = s0;
+          float sv = 0.f;
+#pragma unroll
+          for (int w = 0; w < kTeamWaves; ++w) {
+            const float* pr = lds + L.PART + (w * S + hs) * 16;
+            s0 += *(const f32x4*)pr;
+            s1 += *(const f32x4*)(pr + 4);
+            sv += pr[AMAX];
+          }
+#pragma unroll
+          for (int k = 0; k < AMAX; ++k) out[k] = (k < 4 ? s0[k & 3] : s1[k & 3]) + lds[L.bo + k];
+          vmh = sv;
+        } else
 #pragma unroll
         for (int k = 0; k < AMAX; ++k) {
           f32x4 w0, w1;
@@ -556,8 +607,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
           }
           out[k] = sum8(dot8(w0, w1, ha0, ha1)) + lds[L.bo + k];
         }
-        float vp = 0.f;
-        {
+        float vp = vmh;
+        if (!MH) {
           f32x4 w0, w1;
           if (WREG) {
             w0 = (f32x4){wvh[0], wvh[1], wvh[2], wvh[3]};
@@ -568,7 +619,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
           }
           vp = dot8(w0, w1, hc0, hc1);
         }
-        vp = sum8(vp);
+        if (!MH) vp = sum8(vp);
         const float v = vp + lds[L.bv];
         HEAD_STAMP(0);
         const float adv = sc[2], ret = sc[3];
@@ -676,17 +727,27 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         for (int sb = 0; sb < NSB; ++sb) {
           const float* drow = DOUT + (16 * sb + l15) * SD;
           const float dvs = drow[32];
-          f32x4 dk[NA4D];
+          f32x4 dk[NA4D], dz = (f32x4){0.f, 0.f, 0.f, 0.f};
+          if (MH) {
+            // Wo^T dout on the matrix core: A = this wave's Wo columns, B = the sample's deltas
 #pragma unroll
-          for (int c = 0; c < NA4D; ++c) dk[c] = *(const f32x4*)(drow + 4 * c);
+            for (int t = 0; t < 2; ++t) dz = mfma16(woT[t], drow[4 * t + h4], dz);
+          } else {
+#pragma unroll
+            for (int c = 0; c < NA4D; ++c) dk[c] = *(const f32x4*)(drow + 4 * c);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int col = row0 + 4 * r + h4;  // perm(row0 + 4 h4 + r)
             float acc = 0.f;
+            if (MH) {
+              acc = dz[r];
+            } else {
 #pragma unroll
-            for (int k = 0; k < AMAX; ++k)
-              acc += (WREG ? wod[k < AR ? k : 0][r] : lds[L.Wo + k * H + col]) *
-                     dk[k >> 2][k & 3];  // head-image rows >= A are zero
+              for (int k = 0; k < AMAX; ++k)
+                acc += (WREG ? wod[k < AR ? k : 0][r] : lds[L.Wo + k * H + col]) *
+                       dk[k >> 2][k & 3];  // head-image rows >= A are zero
+            }
             const float y = har[sb][r];
             dza[sb][r] = acc * (1.0f - y * y);
             const float yc = hcr[sb][r];
