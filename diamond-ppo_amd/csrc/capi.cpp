@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -74,7 +75,8 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
-  unsigned* arrivals = nullptr;  // reduce_adam_kernel's monotonic grid-arrival counter
+  unsigned* arrivals = nullptr;  // [3][kArrivalWords]: reduce_adam_kernel, fused tail x 2
+  unsigned fused_epoch = 0;      // launches of the fused minibatch kernel with the Adam tail
   unsigned radam_epoch = 0;      // reduce_adam launches so far on this handle
   // [E][B] permutations the minibatch kernels gather with, and the Fisher-Yates targets they are
   // resolved from (dppo_learn_targets_f32); double-buffered so the next learn's upload can run
@@ -457,6 +459,35 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
         ga.p_total = h->layout.total;
         int G = mb_grid(mb);
         if (G > h->G) G = h->G;
+        // DPPO_FUSED_ADAM=1: the slab reduction, clip and Adam as the minibatch kernel's own
+        // tail (one launch per minibatch, two grid fan-ins).  Measured: the tail costs what
+        // reduce_adam_kernel does (~8 us: the fan-ins, not the launch, dominate), throughput
+        // within ~1.5 %; the separate kernel stays the default (and keeps the minibatch kernel's
+        // roofline its own).
+        const bool fused_tail = std::getenv("DPPO_FUSED_ADAM") != nullptr;
+        if (fused_tail) {
+          FusedAdam fa{};
+          fa.grad = h->grad;
+          fa.sq_part = h->sq_part;
+          fa.arrivals = h->arrivals + kArrivalWords;
+          fa.epoch = ++h->fused_epoch;
+          fa.params = params;
+          fa.m = adam_m;
+          fa.v = adam_v;
+          fa.max_norm = hp->grad_norm_clip;
+          fa.neg_step_size = (float)(-step_size);
+          fa.bc2_sqrt = (float)bc2_sqrt;
+          fa.beta1 = hp->adam_beta1;
+          fa.beta2 = hp->adam_beta2;
+          fa.eps = hp->adam_eps;
+          fa.trace = trace;
+          fa.ls_off = h->po.ls;
+          fa.ls_n = d.continuous ? d.act_dim : 0;
+          fa.add_entropy_const = d.continuous ? 1 : 0;
+          Timed tm(h, K_GRAD, s);
+          DPPO_TRY(launch_mb(h->sh, h->po, ga, G, s, &fa));
+          continue;
+        }
         {
           Timed tm(h, K_GRAD, s);
           DPPO_TRY(launch_mb(h->sh, h->po, ga, G, s));
@@ -566,7 +597,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
-  chk(dalloc(&h->arrivals, kArrivalWords));
+  chk(dalloc(&h->arrivals, 3 * kArrivalWords));
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->B));
     chk(dalloc(&h->targets_dev2[k], E * h->B));
@@ -597,7 +628,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   if (rc == DPPO_OK) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
-    (void)hipMemset(h->arrivals, 0, kArrivalWords * sizeof(unsigned));
+    (void)hipMemset(h->arrivals, 0, 3 * kArrivalWords * sizeof(unsigned));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }

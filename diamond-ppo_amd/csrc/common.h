@@ -101,6 +101,65 @@ int launch_pack(const PackArgs& a, hipStream_t s);
 // (blockIdx % 8), [32 * 9] the release word; each on its own 128-B line
 constexpr int kArrivalWords = 32 * 10;
 
+// ---- optimizer element ops shared by optim.hip and the fused minibatch kernel's tail
+// adam_elem on registers (same operations, same order)
+__device__ __forceinline__ void adam_regs(float& p, float gr, float& mk, float& vk, float coef,
+                                          float w1, float w2, float beta2, float bc2_sqrt,
+                                          float eps, float neg_step_size) {
+#pragma clang fp contract(off)
+  const float g = gr * coef;
+  mk = mk + w1 * (g - mk);
+  vk = vk * beta2;
+  vk = vk + (w2 * g) * g;
+  const float denom = sqrtf(vk) / bc2_sqrt + eps;
+  p = p + neg_step_size * (mk / denom);
+}
+
+__device__ __forceinline__ float clip_coef(double sumsq, float max_norm, float* norm_out) {
+  const float norm = (float)sqrt(sumsq);
+  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1, always applied (clip_grad.py:165-169)
+  float coef = max_norm / (norm + 1e-6f);
+  *norm_out = norm;
+  return coef < 1.0f ? coef : 1.0f;
+}
+
+// s_pi, s_v, s_h: the loss slots {sum l_pi, sum l_v, sum H} that follow the gradient
+__device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v, float s_h,
+                                            float norm, float inv_m, float vf, float ent) {
+  const float lpi = s_pi * inv_m;
+  const float lv = s_v * inv_m;
+  const float h = s_h * inv_m;
+  trace[0] = lpi + vf * lv - ent * h;  // ppo.py:276-280
+  trace[1] = lpi;
+  trace[2] = lv;
+  trace[3] = h;
+  trace[4] = norm;
+}
+
+// Grid-wide fan-in by thread 0 of each workgroup (the grid must be resident): arrive on the
+// counter of this block's XCD group (blockIdx % 8), the last arriver of a group adds to the top
+// counter, the last of those writes the release word that every block polls.  Counters are
+// monotonic: launch `epoch` (1, 2, ...) waits for epoch x arrivals.  The caller drains its
+// publishing stores (vmcnt(0)) before, and reads handed-off data with sc1 loads after.
+__device__ __forceinline__ void grid_fanin(unsigned* ctr, unsigned epoch) {
+  const unsigned x = blockIdx.x & 7;
+  const unsigned nx = (gridDim.x - x + 7) / 8;
+  const unsigned ng = gridDim.x < 8 ? gridDim.x : 8;
+  unsigned* rel = ctr + 32 * 9;
+  const unsigned o1 =
+      __hip_atomic_fetch_add(ctr + 32 * (1 + x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (o1 == epoch * nx - 1) {
+    const unsigned o2 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o2 == epoch * ng - 1) __hip_atomic_store(rel, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int spins = 0;
+       (int)(__hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0;
+       ++spins) {
+    if (spins > (1 << 22)) break;  // never expected: the grid is resident
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Default actor-critic MLP (hidden 64) kernels: mlp.hip.
 struct MlpShape {
   int D, D8, A, continuous, R;  // R = record stride (floats)
@@ -122,11 +181,27 @@ struct GradArgs {
   int64_t slab_stride; // floats per slab (param total + 8 loss slots, rounded)
   int64_t p_total;
 };
+// Single-device tail of the fused minibatch kernel: slab reduction, clip_grad_norm_ and Adam in
+// the same launch (two grid-wide fan-ins instead of a second launch), see mbstep.hip.
+struct FusedAdam {
+  float* grad;          // [p_total + 8] reduced gradient + loss slots (published sc1)
+  double* sq_part;      // [nblk] per-64-parameter-block sums of squares
+  unsigned* arrivals;   // 2 x kArrivalWords (two fan-ins)
+  unsigned epoch;       // launch number (monotonic counters, never reset)
+  float* params;        // updated in place
+  float* m;
+  float* v;
+  float max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps;
+  float* trace;         // [5] {loss, l_pi, l_v, H, norm} of this minibatch
+  int64_t ls_off;       // continuous: log-std parameters get -entropy_beta added (optim.hip)
+  int ls_n;
+  int add_entropy_const;
+};
 // Feature-split fused minibatch kernel (mbstep.hip), the one learn() uses.
 size_t mb_lds_bytes(const MlpShape& sh);
 int mb_grid(int32_t m);
 int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
-              hipStream_t s);
+              hipStream_t s, const FusedAdam* fused = nullptr);
 
 // Optimiser kernels: optim.hip.
 int slab_reduce_blocks(int64_t p_total);

@@ -113,7 +113,96 @@ struct MArgs {
   float* slabs;
   int64_t slab_stride, p_total;
   int D, D8, D16, A, R;
+  int fuse;      // single device: the slab reduction, clip and Adam run in this launch's tail
+  int nblk;      // 64-parameter blocks of the tail (slab_reduce_blocks)
+  FusedAdam fa;
 };
+
+constexpr int kTailParams = 64;  // parameters per tail block (= optim.hip's kRedParams)
+
+// Tail of a single-device launch (replaces reduce_adam_kernel and its launch): every workgroup's
+// slab is published (sc1 stores, drained); after a grid fan-in workgroup b reduces parameter
+// blocks b, b + G, ... over all G slabs (sc1 loads, wave w takes slabs w, w + 8, ...; the wave
+// partials are combined in a fixed order), publishes them and each block's sum of squares; after
+// a second fan-in every workgroup sums the block squares in the same order (global norm,
+// clip_grad.py:165-169) and applies Adam (torch _single_tensor_adam op order) to its blocks.
+__device__ void fused_reduce_adam(const MArgs& a, float* lds) {
+#pragma clang fp contract(off)
+  const FusedAdam& f = a.fa;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = kThreads / 64;
+  const int G = gridDim.x;
+  const int64_t n = a.p_total + 8;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are complete
+  __syncthreads();
+  if (tid == 0) grid_fanin(f.arrivals, f.epoch);
+  __syncthreads();
+  for (int blk = blockIdx.x; blk < a.nblk; blk += G) {
+    const int64_t p = (int64_t)blk * kTailParams + lane;
+    float sacc = 0.0f;
+    if (p < n) {
+      const float* src = a.slabs + p;
+      int g = wave;
+      for (; g + 15 * NW < G; g += 16 * NW) {
+        float x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          x[k] = __hip_atomic_load(src + (int64_t)(g + NW * k) * a.slab_stride, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc += x[k];
+      }
+      for (; g < G; g += NW)
+        sacc += __hip_atomic_load(src + (int64_t)g * a.slab_stride, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
+    lds[wave * 64 + lane] = sacc;
+    __syncthreads();
+    if (wave == 0) {
+      float t = 0.0f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += lds[w * 64 + lane];
+      // d(-beta * mean H)/d log_std = -beta per action dim (continuous_ppo.py:286-291)
+      if (f.add_entropy_const && p >= f.ls_off && p < f.ls_off + f.ls_n) t -= a.ent;
+      if (p < n) __hip_atomic_store(f.grad + p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double q = (p < a.p_total) ? (double)t * (double)t : 0.0;
+      for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+      if (lane == 0)
+        __hip_atomic_store(f.sq_part + blk, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // lds reused by the next block
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) grid_fanin(f.arrivals + kArrivalWords, f.epoch);
+  __syncthreads();
+  if (wave != 0) return;
+  double sq = 0.0;
+  for (int k = lane; k < a.nblk; k += 64)
+    sq += __hip_atomic_load(f.sq_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+  float norm;
+  const float coef = clip_coef(sq, f.max_norm, &norm);
+  for (int blk = blockIdx.x; blk < a.nblk; blk += G) {
+    const int64_t p = (int64_t)blk * kTailParams + lane;
+    if (p < a.p_total) {
+      float pk = f.params[p], mk = f.m[p], vk = f.v[p];
+      const float gk = __hip_atomic_load(f.grad + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      adam_regs(pk, gk, mk, vk, coef, 1.0f - f.beta1, 1.0f - f.beta2, f.beta2, f.bc2_sqrt, f.eps,
+                f.neg_step_size);
+      f.params[p] = pk;
+      f.m[p] = mk;
+      f.v[p] = vk;
+    }
+  }
+  if (blockIdx.x == 0 && lane == 0 && f.trace) {
+    const float* ls = f.grad + a.p_total;
+    write_trace(f.trace, __hip_atomic_load(ls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(ls + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                __hip_atomic_load(ls + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), norm,
+                a.inv_m, a.vf, a.ent);
+  }
+}
 
 inline int a4(int x) { return (x + 3) & ~3; }
 
@@ -924,6 +1013,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     }
     __syncthreads();  // pairs with the forward team's head-partial rendezvous
   }
+  if (a.fuse) fused_reduce_adam(a, lds_);
 }
 
 }  // namespace
@@ -955,7 +1045,7 @@ int mb_grid(int32_t m) {
 }
 
 int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, int G,
-              hipStream_t s) {
+              hipStream_t s, const FusedAdam* fused) {
   MArgs k{};
   const int D16 = (sh.D + 15) / 16 * 16;
   k.L = make_lds2(D16);
@@ -976,6 +1066,11 @@ int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, in
   k.D16 = D16;
   k.A = sh.A;
   k.R = sh.R;
+  if (fused) {
+    k.fuse = 1;
+    k.fa = *fused;
+    k.nblk = (int)((ga.p_total + 8 + kTailParams - 1) / kTailParams);
+  }
   size_t lds = (size_t)k.L.total * sizeof(float);
   // the epilogue reuses the step images: team-1 accumulators + per-wave head partials
   const size_t epi = (size_t)(kTeamWaves * (16 + 3) * 64) * sizeof(float);  // head partials

@@ -100,40 +100,6 @@ __device__ __forceinline__ void adam_elem(float* __restrict__ params, const floa
   v[k] = vk;
 }
 
-// adam_elem on registers (same operations, same order)
-__device__ __forceinline__ void adam_regs(float& p, float gr, float& mk, float& vk, float coef,
-                                          float w1, float w2, float beta2, float bc2_sqrt,
-                                          float eps, float neg_step_size) {
-#pragma clang fp contract(off)
-  const float g = gr * coef;
-  mk = mk + w1 * (g - mk);
-  vk = vk * beta2;
-  vk = vk + (w2 * g) * g;
-  const float denom = sqrtf(vk) / bc2_sqrt + eps;
-  p = p + neg_step_size * (mk / denom);
-}
-
-__device__ __forceinline__ float clip_coef(double sumsq, float max_norm, float* norm_out) {
-  const float norm = (float)sqrt(sumsq);
-  // clip_coef = max_norm / (total_norm + 1e-6), clamped to 1, always applied (clip_grad.py:165-169)
-  float coef = max_norm / (norm + 1e-6f);
-  *norm_out = norm;
-  return coef < 1.0f ? coef : 1.0f;
-}
-
-// s_pi, s_v, s_h: the loss slots {sum l_pi, sum l_v, sum H} that follow the gradient
-__device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v, float s_h,
-                                            float norm, float inv_m, float vf, float ent) {
-  const float lpi = s_pi * inv_m;
-  const float lv = s_v * inv_m;
-  const float h = s_h * inv_m;
-  trace[0] = lpi + vf * lv - ent * h;  // ppo.py:276-280
-  trace[1] = lpi;
-  trace[2] = lv;
-  trace[3] = h;
-  trace[4] = norm;
-}
-
 // grad: [n] flat gradient followed by 8 loss slots {sum l_pi, sum l_v, sum H, ...}.
 // sq_part/n_sq: per-block partial sums of squares of grad (null => recompute from grad).
 __global__ __launch_bounds__(256) void clip_adam_kernel(

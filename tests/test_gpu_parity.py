@@ -148,12 +148,18 @@ def flat_params(agent):
     return np.concatenate([p.detach().cpu().numpy().ravel() for p in agent.network.parameters()])
 
 
-@pytest.mark.parametrize("name,device_shuffle",
-                         [(n, False) for n in LEARN_TRACES] + [("cartpole_decay", True),
-                                                               ("cheetah_small", True)])
-def test_learn_matches_reference_trace(name, device_shuffle):
+@pytest.mark.parametrize("name,device_shuffle,fused_adam",
+                         [(n, False, False) for n in LEARN_TRACES] +
+                         [("cartpole_decay", True, False), ("cheetah_small", True, False),
+                          ("lunar_medium", False, True), ("cheetah_small", False, True)])
+def test_learn_matches_reference_trace(name, device_shuffle, fused_adam, monkeypatch):
     """Full drop-in learn() through the fused HIP path vs the reference's captured trace,
-    including the NumPy-RNG minibatch order (global RNG set to the captured state)."""
+    including the NumPy-RNG minibatch order (global RNG set to the captured state); also with the
+    slab reduction + clip + Adam as the minibatch kernel's tail (DPPO_FUSED_ADAM=1)."""
+    if fused_adam:
+        monkeypatch.setenv("DPPO_FUSED_ADAM", "1")
+    else:
+        monkeypatch.delenv("DPPO_FUSED_ADAM", raising=False)
     z = load_golden(f"learn_{name}.npz")
     T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
     agent = make_agent(z)
