@@ -151,15 +151,21 @@ def flat_params(agent):
 @pytest.mark.parametrize("name,device_shuffle,fused_adam",
                          [(n, False, False) for n in LEARN_TRACES] +
                          [("cartpole_decay", True, False), ("cheetah_small", True, False),
-                          ("lunar_medium", False, True), ("cheetah_small", False, True)])
+                          ("lunar_medium", False, True), ("cheetah_small", False, True),
+                          ("cartpole_small", False, "split"), ("lunar_medium", False, "split"),
+                          ("cheetah_small", False, "split"), ("pendulum_medium", False, "split")])
 def test_learn_matches_reference_trace(name, device_shuffle, fused_adam, monkeypatch):
     """Full drop-in learn() through the fused HIP path vs the reference's captured trace,
     including the NumPy-RNG minibatch order (global RNG set to the captured state); also with the
-    slab reduction + clip + Adam as the minibatch kernel's tail (DPPO_FUSED_ADAM=1)."""
-    if fused_adam:
+    slab reduction + clip + Adam as the minibatch kernel's tail (DPPO_FUSED_ADAM=1), and with the
+    multi-GPU per-minibatch sequence (minibatch kernel -> slab_reduce_kernel -> [RCCL] ->
+    clip_adam_kernel) forced on one device (DPPO_SPLIT_ADAM=1)."""
+    monkeypatch.delenv("DPPO_FUSED_ADAM", raising=False)
+    monkeypatch.delenv("DPPO_SPLIT_ADAM", raising=False)
+    if fused_adam == "split":
+        monkeypatch.setenv("DPPO_SPLIT_ADAM", "1")
+    elif fused_adam:
         monkeypatch.setenv("DPPO_FUSED_ADAM", "1")
-    else:
-        monkeypatch.delenv("DPPO_FUSED_ADAM", raising=False)
     z = load_golden(f"learn_{name}.npz")
     T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
     agent = make_agent(z)
