@@ -9,6 +9,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -47,6 +52,25 @@ ParamOffsets offsets_from_layout(const dppo_dims& d, const dppo_layout& L) {
 }  // namespace dppo
 
 using namespace dppo;
+
+struct dppo_handle;
+
+// Single-device loopback group (dppo_loopback_group): n handles on ONE device, one per rank, whose
+// learns are driven concurrently from n host threads on n streams.  Each all-reduce of the
+// data-parallel path becomes: record "ready" on the rank's stream, host barrier, wait for every
+// peer's "ready", sum the n buffers in rank order into a private scratch (rank_sum_kernel), record
+// "done", host barrier, wait for every peer's "done" (nobody still reads this rank's buffer), copy
+// the sum back.  RCCL refuses two ranks on one GPU; this is how the N > 1 data path
+// (statistics / gradient exchange, global divisors, rank-0-only terms) is parity-tested on one.
+struct LoopGroup {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  dppo_handle* members[kMaxLoopRanks] = {};
+  void* bufs[kMaxLoopRanks] = {};
+};
 
 #define DPPO_NCCL_CHECK(expr)                                                             \
   do {                                                                                    \
@@ -108,6 +132,11 @@ struct dppo_handle {
   // RCCL
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // single-device loopback group (tests): shared by its members
+  std::shared_ptr<LoopGroup> loop;
+  void* loop_out = nullptr;
+  size_t loop_bytes = 0;
+  hipEvent_t loop_ready = nullptr, loop_done = nullptr;
 };
 
 namespace {
@@ -257,8 +286,54 @@ int require_mlp(const dppo_handle* h) {
   return DPPO_OK;
 }
 
+// ranks taking part in the exchanges (RCCL communicator or loopback group), else 1
+inline bool distributed(const dppo_handle* h) { return (h->comm || h->loop) && h->nranks > 1; }
+inline int world_of(const dppo_handle* h) { return distributed(h) ? h->nranks : 1; }
+
+int loop_barrier(LoopGroup* g) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  const uint64_t gen = g->gen;
+  if (++g->arrived == g->n) {
+    g->arrived = 0;
+    ++g->gen;
+    g->cv.notify_all();
+    return DPPO_OK;
+  }
+  if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->gen != gen; })) {
+    set_error("loopback group: a rank did not reach the all-reduce within 120 s");
+    return DPPO_ECOMM;
+  }
+  return DPPO_OK;
+}
+
+int loop_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s) {
+  LoopGroup* g = h->loop.get();
+  const size_t bytes = n * (f64 ? sizeof(double) : sizeof(float));
+  if (bytes > h->loop_bytes) {
+    set_error("loopback all-reduce of %zu bytes exceeds the %zu-byte scratch", bytes,
+              h->loop_bytes);
+    return DPPO_EINVAL;
+  }
+  g->bufs[h->rank] = buf;
+  DPPO_HIP_CHECK(hipEventRecord(h->loop_ready, s));
+  DPPO_TRY(loop_barrier(g));
+  RankPtrs src{};
+  for (int r = 0; r < g->n; ++r) {
+    src.p[r] = g->bufs[r];
+    if (r != h->rank) DPPO_HIP_CHECK(hipStreamWaitEvent(s, g->members[r]->loop_ready, 0));
+  }
+  DPPO_TRY(launch_rank_sum(src, g->n, h->loop_out, (int64_t)n, f64, s));
+  DPPO_HIP_CHECK(hipEventRecord(h->loop_done, s));
+  DPPO_TRY(loop_barrier(g));
+  for (int r = 0; r < g->n; ++r)
+    if (r != h->rank) DPPO_HIP_CHECK(hipStreamWaitEvent(s, g->members[r]->loop_done, 0));
+  DPPO_HIP_CHECK(hipMemcpyAsync(buf, h->loop_out, bytes, hipMemcpyDeviceToDevice, s));
+  return DPPO_OK;
+}
+
 int allreduce(dppo_handle* h, void* buf, size_t n, ncclDataType_t t, hipStream_t s) {
-  if (!h->comm || h->nranks <= 1) return DPPO_OK;
+  if (!distributed(h)) return DPPO_OK;
+  if (h->loop) return loop_allreduce(h, buf, n, t == ncclFloat64, s);
   DPPO_NCCL_CHECK(ncclAllReduce(buf, buf, n, t, ncclSum, h->comm, s));
   return DPPO_OK;
 }
@@ -291,7 +366,7 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
       Timed tm(h, K_STATS, s);
       DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, s));
     }
-    if (h->comm && h->nranks > 1) {
+    if (distributed(h)) {
       Timed tm(h, K_COMM, s, true);
       DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, s));
     }
@@ -304,7 +379,7 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
   pa.adv = h->adv;
   pa.ret = h->ret;
   pa.dsum = h->dsum;
-  pa.n_total = (double)h->B * (double)(h->comm ? h->nranks : 1);
+  pa.n_total = (double)h->B * (double)world_of(h);
   pa.advantage_norm = hp->advantage_norm;
   pa.adv_out = h->adv_n;
   pa.rec = h->rec;
@@ -363,7 +438,7 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int3
                                 h->po.ls, d.continuous ? d.act_dim : 0, hp->entropy_beta,
                                 (d.continuous && h->rank == 0) ? 1 : 0, s));
   }
-  if (h->comm && h->nranks > 1) {
+  if (distributed(h)) {
     Timed tm(h, K_COMM, s, true);
     DPPO_TRY(allreduce(h, h->grad, (size_t)h->layout.total + 8, ncclFloat32, s));
   }
@@ -430,7 +505,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
   }
   // (6) E x M dependent optimizer steps (ppo.py:258-285)
   const int32_t mb = h->mb;
-  const int32_t m_total = mb * (h->comm ? h->nranks : 1);
+  const int32_t m_total = mb * world_of(h);
   const float inv_m = (float)(1.0 / (double)m_total);
   for (int64_t e = 0; e < E; ++e) {
     for (int64_t j = 0; j < M; ++j) {
@@ -445,7 +520,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
       // DPPO_SPLIT_ADAM=1 (parity tests): the multi-rank sequence -- minibatch kernel, slab
       // reduction, [all-reduce], clip + Adam kernel -- on one device, so the N > 1 kernels are
       // checked against the reference traces without a second GPU
-      const bool multi = (h->comm && h->nranks > 1) || std::getenv("DPPO_SPLIT_ADAM") != nullptr;
+      const bool multi = distributed(h) || std::getenv("DPPO_SPLIT_ADAM") != nullptr;
       if (!multi) {
         // single device: fused kernel -> slab reduce + clip + Adam in one launch
         GradArgs ga{};
@@ -648,6 +723,9 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
   if (h->comm) ncclCommDestroy(h->comm);
+  if (h->loop_out) (void)hipFree(h->loop_out);
+  if (h->loop_ready) (void)hipEventDestroy(h->loop_ready);
+  if (h->loop_done) (void)hipEventDestroy(h->loop_done);
   (void)hipFree(h->logp);
   (void)hipFree(h->values);
   (void)hipFree(h->next_values);
@@ -701,7 +779,7 @@ int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream) {
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, S(stream)));
   DPPO_TRY(allreduce(h, h->dsum, 2, ncclFloat64, S(stream)));
-  const double n = (double)h->B * (double)(h->comm ? h->nranks : 1);
+  const double n = (double)h->B * (double)world_of(h);
   return launch_stats_finalize(h->dsum, n, mean_std, S(stream));
 }
 
@@ -900,6 +978,35 @@ int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id1
   h->comm = c;
   h->nranks = nranks;
   h->rank = rank;
+  return DPPO_OK;
+}
+
+int dppo_loopback_group(dppo_handle** hs, int32_t n) {
+  if (!hs || n < 2 || n > kMaxLoopRanks) {
+    set_error("dppo_loopback_group: need 2..%d handles", kMaxLoopRanks);
+    return DPPO_EINVAL;
+  }
+  for (int r = 0; r < n; ++r) {
+    dppo_handle* h = hs[r];
+    if (!h || h->device != hs[0]->device || h->nranks != n || h->rank != r || h->comm ||
+        h->loop || h->layout.total != hs[0]->layout.total) {
+      set_error("dppo_loopback_group: handle %d must be rank %d of world_size %d on device %d, "
+                "same parameter layout, no communicator or group yet", r, r, n, hs[0]->device);
+      return DPPO_EINVAL;
+    }
+  }
+  auto g = std::make_shared<LoopGroup>();
+  g->n = n;
+  for (int r = 0; r < n; ++r) {
+    dppo_handle* h = hs[r];
+    DPPO_HIP_CHECK(hipSetDevice(h->device));
+    h->loop_bytes = std::max<size_t>((size_t)h->slab_stride * sizeof(float), 4 * sizeof(double));
+    DPPO_HIP_CHECK(hipMalloc(&h->loop_out, h->loop_bytes));
+    DPPO_HIP_CHECK(hipEventCreateWithFlags(&h->loop_ready, hipEventDisableTiming));
+    DPPO_HIP_CHECK(hipEventCreateWithFlags(&h->loop_done, hipEventDisableTiming));
+    g->members[r] = h;
+  }
+  for (int r = 0; r < n; ++r) hs[r]->loop = g;
   return DPPO_OK;
 }
 

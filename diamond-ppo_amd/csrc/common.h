@@ -223,6 +223,14 @@ int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p
 int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, float max_norm,
                      float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
                      float* out_norm, hipStream_t s);
+// out[i] = src[0][i] + src[1][i] + ... + src[n-1][i] in rank order (f32 or f64 when `f64`); the
+// device-local stand-in for the RCCL sum of a single-device loopback group (capi.cpp)
+constexpr int kMaxLoopRanks = 8;
+struct RankPtrs {
+  const void* p[kMaxLoopRanks];
+};
+int launch_rank_sum(const RankPtrs& src, int n, void* out, int64_t count, bool f64,
+                    hipStream_t s);
 
 // Fisher-Yates resolution (shuffle.hip): perms[c][n] from swap targets[c][n];
 // scratch = 3 * count * n int32.

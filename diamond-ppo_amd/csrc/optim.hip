@@ -240,7 +240,33 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
   }
 }
 
+template <typename F>
+__global__ __launch_bounds__(256) void rank_sum_kernel(RankPtrs src, int n, F* __restrict__ out,
+                                                       int64_t count) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    F acc = ((const F*)src.p[0])[i];
+    for (int r = 1; r < n; ++r) acc += ((const F*)src.p[r])[i];
+    out[i] = acc;
+  }
+}
+
 }  // namespace
+
+int launch_rank_sum(const RankPtrs& src, int n, void* out, int64_t count, bool f64,
+                    hipStream_t s) {
+  int64_t g = (count + 255) / 256;
+  if (g > 256) g = 256;
+  if (g < 1) g = 1;
+  if (f64)
+    DPPO_LAUNCH(rank_sum_kernel<double>, dim3((unsigned)g), dim3(256), 0, s, src, n,
+                (double*)out, count);
+  else
+    DPPO_LAUNCH(rank_sum_kernel<float>, dim3((unsigned)g), dim3(256), 0, s, src, n,
+                (float*)out, count);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
 
 int slab_reduce_blocks(int64_t p_total) { return (int)((p_total + 8 + kRedParams - 1) / kRedParams); }
 

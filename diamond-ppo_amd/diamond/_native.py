@@ -28,7 +28,7 @@ EXPORTED = [
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_resolve", "dppo_act_f32",
+    "dppo_perm_targets_numpy", "dppo_perm_resolve", "dppo_act_f32", "dppo_loopback_group",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
                   "allreduce", "perm", "reduce_adam"]
@@ -110,6 +110,7 @@ def load():
         "dppo_perm_resolve": (ctypes.c_int, [vp, vp, i64, i32, vp, vp]),
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
+        "dppo_loopback_group": (ctypes.c_int, [P(vp), i32]),
         "dppo_set_timing": (ctypes.c_int, [vp, i32]),
         "dppo_get_timing": (ctypes.c_int, [vp, vp, vp]),
     }
@@ -258,6 +259,14 @@ class Handle:
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         buf = ctypes.create_string_buffer(uid, 128)
         check(self.lib.dppo_comm_init(self.h, int(nranks), int(rank), buf), "dppo_comm_init")
+
+
+def loopback_group(handles) -> None:
+    """Join handles (rank r = handles[r], one device) into a loopback group: their concurrent
+    dppo_learn_f32 calls exchange what RCCL would carry, summed on the device (parity tests of
+    the data-parallel path on one GPU)."""
+    arr = (ctypes.c_void_p * len(handles))(*[h.h.value for h in handles])
+    check(load().dppo_loopback_group(arr, len(handles)), "dppo_loopback_group")
 
 
 def comm_unique_id() -> bytes:

@@ -226,6 +226,13 @@ int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t
 int dppo_comm_unique_id(char* out128);
 int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128);
 
+/* Single-device loopback group (parity tests of the data-parallel path without a second GPU;
+ * RCCL refuses two ranks on one device): hs[r] must be rank r of world_size n (dppo_dims), all on
+ * one device, n <= 8.  Their dppo_learn_f32 calls, issued concurrently from n host threads on n
+ * streams, then exchange exactly what RCCL would carry (advantage statistics, per-minibatch
+ * gradient + loss partials), summed in rank order on the device.  Not for production use. */
+int dppo_loopback_group(dppo_handle** hs, int32_t n);
+
 #pragma GCC visibility pop
 
 #ifdef __cplusplus
