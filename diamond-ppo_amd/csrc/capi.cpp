@@ -99,7 +99,13 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
-  unsigned* arrivals = nullptr;  // [3][kArrivalWords]: reduce_adam_kernel, fused tail x 2
+  unsigned* arrivals = nullptr;  // [4][kArrivalWords]: reduce_adam_kernel, fused tail x 2, probe
+  // sticky device error word (grid_fanin timeouts): host-coherent pinned memory and its device
+  // alias; the host reads it at the start of every call on the handle, without a sync
+  unsigned* err_host = nullptr;
+  unsigned* err_dev = nullptr;
+  unsigned long long fanin_ticks = kFaninTimeoutTicks;
+  bool radam_ok = false;  // reduce_adam_kernel's grid fits on the device at once
   unsigned fused_epoch = 0;      // launches of the fused minibatch kernel with the Adam tail
   unsigned radam_epoch = 0;      // reduce_adam launches so far on this handle
   // [E][B] permutations the minibatch kernels gather with, and the Fisher-Yates targets they are
@@ -223,6 +229,19 @@ int dalloc(T** p, int64_t n) {
   } while (0)
 
 inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+// The handle's sticky device error (grid_fanin timeout), read without synchronising: a kernel
+// enqueued earlier reports here once it has run -- at the latest at the first call after the
+// next synchronisation (dppo_get_trace, dppo_status after a sync).
+int device_status(const dppo_handle* h) {
+  const unsigned e = h->err_host ? __atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) : 0u;
+  if (e == 0u) return DPPO_OK;
+  set_error("a grid-wide fan-in timed out (code %u): its workgroups were not all resident on the "
+            "device at once (another process holding the CUs, or a partitioned device); the "
+            "parameters of that optimizer step were left unchanged and this handle is no longer "
+            "usable", e);
+  return DPPO_EHIP;
+}
 
 enum KClass {
   K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_PERM, K_RADAM, K_NCLASS
@@ -479,6 +498,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
     set_error("null argument to dppo_learn_f32");
     return DPPO_EINVAL;
   }
+  DPPO_TRY(device_status(h));
   const dppo_dims& d = h->dims;
   if (h->B % d.num_minibatches != 0) {
     // the reference's perms.reshape(E, M, B // M) raises ValueError (ppo.py:255)
@@ -520,7 +540,9 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
       // DPPO_SPLIT_ADAM=1 (parity tests): the multi-rank sequence -- minibatch kernel, slab
       // reduction, [all-reduce], clip + Adam kernel -- on one device, so the N > 1 kernels are
       // checked against the reference traces without a second GPU
-      const bool multi = distributed(h) || std::getenv("DPPO_SPLIT_ADAM") != nullptr;
+      // A device that cannot hold reduce_adam_kernel's grid at once takes the same sequence.
+      const bool multi =
+          distributed(h) || !h->radam_ok || std::getenv("DPPO_SPLIT_ADAM") != nullptr;
       if (!multi) {
         // single device: fused kernel -> slab reduce + clip + Adam in one launch
         GradArgs ga{};
@@ -549,6 +571,8 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
           fa.sq_part = h->sq_part;
           fa.arrivals = h->arrivals + kArrivalWords;
           fa.epoch = ++h->fused_epoch;
+          fa.err = h->err_dev;
+          fa.timeout_ticks = h->fanin_ticks;
           fa.params = params;
           fa.m = adam_m;
           fa.v = adam_v;
@@ -581,7 +605,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
             d.continuous ? d.act_dim : 0, hp->entropy_beta, d.continuous ? 1 : 0, h->arrivals,
             ++h->radam_epoch, params, adam_m, adam_v, hp->grad_norm_clip, (float)(-step_size), (float)bc2_sqrt,
             hp->adam_beta1, hp->adam_beta2, hp->adam_eps, trace, inv_m, hp->value_loss_weight,
-            hp->entropy_beta, s));
+            hp->entropy_beta, h->err_dev, h->fanin_ticks, s));
         continue;
       }
       DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
@@ -675,7 +699,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->partials, 2 * ((int64_t)(dims->num_envs + 15) / 16 + 1)));
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
-  chk(dalloc(&h->arrivals, 3 * kArrivalWords));
+  chk(dalloc(&h->arrivals, 4 * kArrivalWords));
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->B));
     chk(dalloc(&h->targets_dev2[k], E * h->B));
@@ -691,6 +715,20 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
       rc = DPPO_EHIP;
     }
   }
+  if (rc == DPPO_OK) {
+    if (hipHostMalloc((void**)&h->err_host, 64, hipHostMallocCoherent | hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&h->err_dev, h->err_host, 0) != hipSuccess) {
+      set_error("hipHostMalloc (coherent error word) failed");
+      rc = DPPO_EHIP;
+    } else {
+      __atomic_store_n(h->err_host, 0u, __ATOMIC_RELEASE);
+    }
+  }
+  // The single-device optimizer step waits in a grid-wide fan-in: take it only when its whole
+  // grid fits on the device at once (a partitioned device or an occupancy surprise takes the
+  // three-kernel path -- slab reduce, clip + Adam -- instead, which needs no co-residency).
+  h->radam_ok = reduce_adam_capacity(device) >= reduce_adam_blocks(h->layout.total);
   for (int k = 0; k < 2 && rc == DPPO_OK; ++k) {
     hipError_t e = hipHostMalloc((void**)&h->perms_pinned[k],
                                  (size_t)(E * h->B) * sizeof(int32_t), hipHostMallocDefault);
@@ -706,7 +744,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   if (rc == DPPO_OK) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
-    (void)hipMemset(h->arrivals, 0, 3 * kArrivalWords * sizeof(unsigned));
+    (void)hipMemset(h->arrivals, 0, 4 * kArrivalWords * sizeof(unsigned));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }
@@ -754,6 +792,7 @@ void dppo_destroy(dppo_handle* h) {
     if (h->perm_copy_done[k]) (void)hipEventDestroy(h->perm_copy_done[k]);
   }
   for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
+  if (h->err_host) (void)hipHostFree(h->err_host);
   delete h;
 }
 
@@ -823,8 +862,32 @@ int dppo_prepare_f32(dppo_handle* h, const dppo_rollout* rollout, const float* p
     set_error("null handle");
     return DPPO_EINVAL;
   }
+  DPPO_TRY(device_status(h));
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   return prepare(h, rollout, params, hp, outputs, S(stream));
+}
+
+int dppo_status(dppo_handle* h) {
+  if (!h) {
+    set_error("null handle");
+    return DPPO_EINVAL;
+  }
+  return device_status(h);
+}
+
+int dppo_fanin_selftest(dppo_handle* h, int32_t blocks, int32_t lds_bytes, int64_t timeout_us,
+                        void* stream) {
+  if (!h || blocks < 1 || lds_bytes < 0 || lds_bytes > 160 * 1024 || timeout_us < 1) {
+    set_error("invalid argument to dppo_fanin_selftest");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(device_status(h));
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t s = S(stream);
+  unsigned* ctr = h->arrivals + 3 * kArrivalWords;  // fresh counters: this grid size, epoch 1
+  DPPO_HIP_CHECK(hipMemsetAsync(ctr, 0, kArrivalWords * sizeof(unsigned), s));
+  return launch_fanin_probe(blocks, lds_bytes, ctr, h->err_dev,
+                            (unsigned long long)timeout_us * 100ull, s);
 }
 
 int dppo_minibatch_grad_f32(dppo_handle* h, const float* params, const int32_t* idx, int32_t m,
@@ -834,6 +897,7 @@ int dppo_minibatch_grad_f32(dppo_handle* h, const float* params, const int32_t* 
     set_error("invalid argument to dppo_minibatch_grad_f32");
     return DPPO_EINVAL;
   }
+  DPPO_TRY(device_status(h));
   DPPO_TRY(require_mlp(h));
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t s = S(stream);
@@ -948,6 +1012,7 @@ int dppo_get_trace(dppo_handle* h, float* host_out, int32_t rows) {
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   DPPO_HIP_CHECK(hipStreamSynchronize(h->last_stream));
+  DPPO_TRY(device_status(h));
   DPPO_HIP_CHECK(hipMemcpy(host_out, h->trace, (size_t)rows * DPPO_TRACE_FIELDS * sizeof(float),
                            hipMemcpyDeviceToHost));
   return DPPO_OK;

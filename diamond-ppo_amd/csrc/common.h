@@ -136,12 +136,28 @@ __device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v,
   trace[4] = norm;
 }
 
-// Grid-wide fan-in by thread 0 of each workgroup (the grid must be resident): arrive on the
-// counter of this block's XCD group (blockIdx % 8), the last arriver of a group adds to the top
-// counter, the last of those writes the release word that every block polls.  Counters are
-// monotonic: launch `epoch` (1, 2, ...) waits for epoch x arrivals.  The caller drains its
-// publishing stores (vmcnt(0)) before, and reads handed-off data with sc1 loads after.
-__device__ __forceinline__ void grid_fanin(unsigned* ctr, unsigned epoch) {
+// Sticky device-side error word of a handle: host-coherent pinned memory (hipHostMallocCoherent,
+// mapped), written by kernels with system-scope vector stores and read by the host at the start
+// of the next C-ABI call without any synchronisation (capi.cpp device_status).
+constexpr unsigned kErrFaninTimeout = 1u;  // a grid-wide fan-in gave up waiting: grid not resident
+// Default bound of one fan-in wait, in s_memrealtime ticks (100 MHz): 5 s.  A resident grid
+// arrives within microseconds; only a grid that is NOT co-resident (another process holding CUs
+// with a long kernel, a partitioned device) can wait this long.
+constexpr unsigned long long kFaninTimeoutTicks = 500000000ull;
+
+// Grid-wide fan-in by thread 0 of each workgroup: arrive on the counter of this block's XCD group
+// (blockIdx % 8), the last arriver of a group adds to the top counter, the last of those writes
+// the release word that every block polls.  Counters are monotonic: launch `epoch` (1, 2, ...)
+// waits for epoch x arrivals.  The caller drains its publishing stores (vmcnt(0)) before, and
+// reads handed-off data with sc1 loads after.
+//
+// Returns false -- and sets *err to kErrFaninTimeout -- when the release has not come after
+// `timeout_ticks` of wall clock, or as soon as *err is already set (an earlier fan-in of this
+// handle failed: queued launches then drain in ~256 polls each instead of waiting out their own
+// timeouts).  The caller must then NOT use the handed-off data.  Every block reaches an exit:
+// the grid always drains, resident or not.
+__device__ __forceinline__ bool grid_fanin(unsigned* ctr, unsigned epoch,
+                                           unsigned long long timeout_ticks, unsigned* err) {
   const unsigned x = blockIdx.x & 7;
   const unsigned nx = (gridDim.x - x + 7) / 8;
   const unsigned ng = gridDim.x < 8 ? gridDim.x : 8;
@@ -152,12 +168,19 @@ __device__ __forceinline__ void grid_fanin(unsigned* ctr, unsigned epoch) {
     const unsigned o2 = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (o2 == epoch * ng - 1) __hip_atomic_store(rel, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (int spins = 0;
-       (int)(__hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0;
-       ++spins) {
-    if (spins > (1 << 22)) break;  // never expected: the grid is resident
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned k = 0;
+       (int)(__hip_atomic_load(rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - epoch) < 0; ++k) {
     __builtin_amdgcn_s_sleep(1);
+    if ((k & 255u) == 255u) {
+      const bool late = __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks;
+      if (late || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        __hip_atomic_store(err, kErrFaninTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
   }
+  return true;
 }
 
 // Default actor-critic MLP (hidden 64) kernels: mlp.hip.
@@ -188,6 +211,8 @@ struct FusedAdam {
   double* sq_part;      // [nblk] per-64-parameter-block sums of squares
   unsigned* arrivals;   // 2 x kArrivalWords (two fan-ins)
   unsigned epoch;       // launch number (monotonic counters, never reset)
+  unsigned* err;        // sticky device error word (host-coherent), see grid_fanin
+  unsigned long long timeout_ticks;
   float* params;        // updated in place
   float* m;
   float* v;
@@ -213,13 +238,21 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
                             float bc2_sqrt, float beta1, float beta2, float eps, float* out_norm,
                             float* trace, float inv_m, float vf, float ent, hipStream_t s);
 // slab reduce + clip + Adam fused (single device): `arrivals` = a device counter zeroed once;
-// launch number `epoch` (1, 2, ...) on it waits for epoch x blocks arrivals
+// launch number `epoch` (1, 2, ...) on it waits for epoch x blocks arrivals.  On a fan-in timeout
+// (grid_fanin) the blocks leave their parameters untouched and set *err.
 int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p_total, float* grad,
                        double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
                        int add_entropy_const, unsigned* arrivals, unsigned epoch, float* params,
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
-                       float ent, hipStream_t s);
+                       float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s);
+// Workgroups of reduce_adam_kernel that fit on the device at once (occupancy x CUs).
+int reduce_adam_capacity(int device);
+int reduce_adam_blocks(int64_t p_total);
+// Fan-in self test (dppo_fanin_selftest): `blocks` workgroups of 1024 threads holding
+// `lds_bytes` of LDS each meet in one grid_fanin on `ctr` (zeroed by the caller, epoch 1).
+int launch_fanin_probe(int blocks, int lds_bytes, unsigned* ctr, unsigned* err,
+                       unsigned long long timeout_ticks, hipStream_t s);
 int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, float max_norm,
                      float neg_step_size, float bc2_sqrt, float beta1, float beta2, float eps,
                      float* out_norm, hipStream_t s);

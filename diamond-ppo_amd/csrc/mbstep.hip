@@ -133,10 +133,14 @@ __device__ void fused_reduce_adam(const MArgs& a, float* lds) {
   constexpr int NW = kThreads / 64;
   const int G = gridDim.x;
   const int64_t n = a.p_total + 8;
+  int* released = (int*)(lds + NW * 64);  // thread 0's fan-in outcome, for the whole block
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are complete
   __syncthreads();
-  if (tid == 0) grid_fanin(f.arrivals, f.epoch);
+  if (tid == 0) *released = grid_fanin(f.arrivals, f.epoch, f.timeout_ticks, f.err) ? 1 : 0;
   __syncthreads();
+  // a timed-out fan-in (grid not co-resident) leaves the parameters untouched; the handle's
+  // sticky error word reports it at the next C-ABI call
+  if (!*released) return;
   for (int blk = blockIdx.x; blk < a.nblk; blk += G) {
     const int64_t p = (int64_t)blk * kTailParams + lane;
     float sacc = 0.0f;
@@ -174,9 +178,10 @@ __device__ void fused_reduce_adam(const MArgs& a, float* lds) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) grid_fanin(f.arrivals + kArrivalWords, f.epoch);
+  if (tid == 0)
+    *released = grid_fanin(f.arrivals + kArrivalWords, f.epoch, f.timeout_ticks, f.err) ? 1 : 0;
   __syncthreads();
-  if (wave != 0) return;
+  if (wave != 0 || !*released) return;
   double sq = 0.0;
   for (int k = lane; k < a.nblk; k += 64)
     sq += __hip_atomic_load(f.sq_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

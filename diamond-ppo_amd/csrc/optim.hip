@@ -140,20 +140,25 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
 // Slab reduction + clip_grad_norm_ + Adam in ONE launch (single device).  Every block reduces its
 // 64 parameters as slab_reduce_kernel does and publishes them and its sum of squares
 // write-through (sc1 stores, the storing wave drained); then all blocks meet in a grid-wide
-// arrival count (a monotonic counter: launch `epoch` waits for epoch x gridDim arrivals, so it is
-// never reset), each acquires (agent scope), sums the per-block squares in a fixed order and
+// fan-in (grid_fanin, common.h: monotonic counters, launch `epoch` waits for epoch x gridDim
+// arrivals, so they are never reset), each sums the per-block squares in a fixed order and
 // applies Adam to its own 64 parameters, whose gradients it still holds in registers and whose
-// moments it prefetched before the wait.  The grid (~210 blocks of 1024 threads) is always
-// resident; the wait is bounded.  (cdna_hip_programming.md Guideline 16 R1; MI355X_MICROARCH.md
-// price list: fanin vs boundary.)
+// moments it prefetched before the wait.  Co-residency of the ~210 blocks of 1024 threads is
+// checked once per handle (reduce_adam_capacity; a device that cannot hold them all takes the
+// three-kernel path instead), and the wait is bounded: a block whose fan-in times out leaves its
+// parameters untouched and raises the handle's sticky error word, which the next C-ABI call
+// reports -- never a silently stale norm.  (cdna_hip_programming.md Guideline 16 R1;
+// MI355X_MICROARCH.md price list: fanin vs boundary.)
 __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     const float* __restrict__ slabs, int G, int64_t stride, int64_t p_total, float* grad,
     double* sq_part, int64_t ls_off, int ls_n, float ent_coef, int add_entropy_const,
     unsigned* arrivals, unsigned epoch, float* __restrict__ params, float* __restrict__ m,
     float* __restrict__ v, float max_norm, float neg_step_size, float bc2_sqrt, float beta1,
-    float beta2, float eps, float* __restrict__ trace, float inv_m, float vf, float ent) {
+    float beta2, float eps, float* __restrict__ trace, float inv_m, float vf, float ent,
+    unsigned* err, unsigned long long timeout_ticks) {
 #pragma clang fp contract(off)
   __shared__ float part[kRedWaves][kRedParams];
+  __shared__ int released;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
   const int64_t n = p_total + 8;
@@ -175,44 +180,13 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains (R1)
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-#ifdef DPPO_ABL_ONECOUNTER
-    __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned* wait_word = arrivals;
-    const unsigned target = epoch * gridDim.x;
-#else
-    // Fan-in sharded by XCD group (blockIdx % 8, one XCD under round-robin dispatch; any
-    // placement is correct): ~G/8 arrivals per counter instead of G serialised atomics on one
-    // word (~13 ns each, MI355X_MICROARCH.md fanin), the last arriver of each group adds to the
-    // top counter, the last of those publishes the release word -- which the waiters poll, so
-    // their loads never queue in front of the arrival atomics.
-    const unsigned x = blockIdx.x & 7;
-    const unsigned nx = (gridDim.x - x + 7) / 8;
-    const unsigned ng = gridDim.x < 8 ? gridDim.x : 8;
-    unsigned* wait_word = arrivals + 32 * 9;
-    const unsigned target = epoch;
-    const unsigned o1 = __hip_atomic_fetch_add(arrivals + 32 * (1 + x), 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    if (o1 == epoch * nx - 1) {
-      const unsigned o2 = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-      if (o2 == epoch * ng - 1)
-        __hip_atomic_store(wait_word, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
-    for (int spins = 0; (int)(__hip_atomic_load(wait_word, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT) - target) < 0;
-         ++spins) {
-      if (spins > (1 << 22)) break;  // never expected: the grid is resident
-      __builtin_amdgcn_s_sleep(1);
-    }
-#ifdef DPPO_ABL_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  }
+  // Fan-in sharded by XCD group (blockIdx % 8, one XCD under round-robin dispatch; any placement
+  // is correct): ~G/8 arrivals per counter instead of G serialised atomics on one word (~13 ns
+  // each, MI355X_MICROARCH.md fanin); the waiters poll a separate release word, so their loads
+  // never queue in front of the arrival atomics.
+  if (threadIdx.x == 0) released = grid_fanin(arrivals, epoch, timeout_ticks, err) ? 1 : 0;
   __syncthreads();
-  if (wave != 0) return;
+  if (wave != 0 || !released) return;
   // Everything read below that other blocks wrote (sq_part, the loss slots) is read with sc1
   // (agent-scope atomic) loads, so no acquire fence (and its L1 invalidate, ~1.5 us per CU) is
   // needed: producer sc1 stores -> vmcnt(0) -> arrival; consumer sees the count -> sc1 loads
@@ -238,6 +212,18 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     const float s_h = __hip_atomic_load(grad + p_total + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     write_trace(trace, s_pi, s_v, s_h, norm, inv_m, vf, ent);
   }
+}
+
+// dppo_fanin_selftest: `gridDim.x` workgroups meet in one grid_fanin; the dynamic LDS they hold
+// only limits how many fit on a CU, so a test can launch a grid that cannot be co-resident.
+__global__ __launch_bounds__(1024) void fanin_probe_kernel(unsigned* ctr, unsigned* err,
+                                                           unsigned long long timeout_ticks) {
+  extern __shared__ float hold[];
+  if (threadIdx.x == 0) {
+    hold[0] = 0.0f;
+    (void)grid_fanin(ctr, 1u, timeout_ticks, err);
+  }
+  __syncthreads();
 }
 
 template <typename F>
@@ -299,11 +285,33 @@ int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p
                        int add_entropy_const, unsigned* arrivals, unsigned epoch, float* params,
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
-                       float ent, hipStream_t s) {
-  DPPO_LAUNCH(reduce_adam_kernel, dim3(slab_reduce_blocks(p_total)), dim3(kRedThreads), 0, s, slabs, G,
+                       float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s) {
+  DPPO_LAUNCH(reduce_adam_kernel, dim3(reduce_adam_blocks(p_total)), dim3(kRedThreads), 0, s, slabs, G,
               slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef, add_entropy_const,
               arrivals, epoch, params, m, v, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
-              trace, inv_m, vf, ent);
+              trace, inv_m, vf, ent, err, timeout_ticks);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+int reduce_adam_blocks(int64_t p_total) { return slab_reduce_blocks(p_total); }
+
+int reduce_adam_capacity(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)reduce_adam_kernel,
+                                                   kRedThreads, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return 0;
+  return per_cu * cus;
+}
+
+int launch_fanin_probe(int blocks, int lds_bytes, unsigned* ctr, unsigned* err,
+                       unsigned long long timeout_ticks, hipStream_t s) {
+  if (lds_bytes < 4) lds_bytes = 4;
+  (void)hipFuncSetAttribute((const void*)fanin_probe_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  DPPO_LAUNCH(fanin_probe_kernel, dim3((unsigned)blocks), dim3(1024), (size_t)lds_bytes, s, ctr,
+              err, timeout_ticks);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

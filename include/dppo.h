@@ -226,6 +226,21 @@ int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t
 int dppo_comm_unique_id(char* out128);
 int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128);
 
+/* Sticky device-side error of the handle, read WITHOUT synchronising (host-coherent word the
+ * kernels write): DPPO_EHIP once a grid-wide fan-in of the single-device optimizer step timed
+ * out (its workgroups were not all resident at once -- another process holding the CUs, a
+ * partitioned device).  The step whose fan-in failed leaves the parameters unchanged; every later
+ * call on the handle (dppo_learn_f32, dppo_get_trace, ...) returns the same error.  No reference
+ * counterpart: clip_grad_norm_ + Adam (ppo.py:284-285) run as host-ordered torch ops there. */
+int dppo_status(dppo_handle* h);
+
+/* Diagnostics: `blocks` workgroups of 1024 threads, each holding `lds_bytes` of LDS, meet in the
+ * same grid-wide fan-in the optimizer step uses, with a `timeout_us` bound.  A grid that fits on
+ * the device completes and leaves the status OK; one that cannot be co-resident drains after the
+ * timeout and sets the sticky error (dppo_status).  Stream-ordered. */
+int dppo_fanin_selftest(dppo_handle* h, int32_t blocks, int32_t lds_bytes, int64_t timeout_us,
+                        void* stream);
+
 /* Single-device loopback group (parity tests of the data-parallel path without a second GPU;
  * RCCL refuses two ranks on one device): hs[r] must be rank r of world_size n (dppo_dims), all on
  * one device, n <= 8.  Their dppo_learn_f32 calls, issued concurrently from n host threads on n

@@ -90,11 +90,11 @@ def normalize_adv(adv):
 # ---------------------------------------------------------------------------------------------
 # Default networks (ppo.py:53-71,84-96; continuous_ppo.py:63-81,95-111)
 # ---------------------------------------------------------------------------------------------
-def _lin(x, W, b):
-    return (x @ W.T + b).astype(f32)
+def _lin(x, W, b, dt=f32):
+    return (x @ W.T + b).astype(dt)
 
 
-def forward(params, x, continuous=False):
+def forward(params, x, continuous=False, dt=f32):
     """Full actor-critic forward; returns the activations the backward needs.
 
     base = tanh(L2(tanh(L1 x)))                       (ppo.py:53-58)
@@ -104,13 +104,13 @@ def forward(params, x, continuous=False):
     value = Lv(tanh(Lc base)).squeeze(-1)             (ppo.py:67-71,95)
     """
     head = "actor_mean_head" if continuous else "actor_head"
-    x = np.asarray(x, f32)
-    h1 = np.tanh(_lin(x, params["base.0.weight"], params["base.0.bias"]))
-    h2 = np.tanh(_lin(h1, params["base.2.weight"], params["base.2.bias"]))
-    ha = np.tanh(_lin(h2, params[f"{head}.0.weight"], params[f"{head}.0.bias"]))
-    out = _lin(ha, params[f"{head}.2.weight"], params[f"{head}.2.bias"])
-    hc = np.tanh(_lin(h2, params["critic_head.0.weight"], params["critic_head.0.bias"]))
-    v = _lin(hc, params["critic_head.2.weight"], params["critic_head.2.bias"])[..., 0]
+    x = np.asarray(x, dt)
+    h1 = np.tanh(_lin(x, params["base.0.weight"], params["base.0.bias"], dt))
+    h2 = np.tanh(_lin(h1, params["base.2.weight"], params["base.2.bias"], dt))
+    ha = np.tanh(_lin(h2, params[f"{head}.0.weight"], params[f"{head}.0.bias"], dt))
+    out = _lin(ha, params[f"{head}.2.weight"], params[f"{head}.2.bias"], dt)
+    hc = np.tanh(_lin(h2, params["critic_head.0.weight"], params["critic_head.0.bias"], dt))
+    v = _lin(hc, params["critic_head.2.weight"], params["critic_head.2.bias"], dt)[..., 0]
     return dict(x=x, h1=h1, h2=h2, ha=ha, hc=hc, out=out, v=v)
 
 
@@ -123,38 +123,38 @@ def values_only(params, x):
     return _lin(hc, params["critic_head.2.weight"], params["critic_head.2.bias"])[..., 0]
 
 
-def log_softmax(z):
+def log_softmax(z, dt=f32):
     """Categorical(logits) normalisation: z - logsumexp(z) (torch distributions/categorical.py:78)."""
-    z = np.asarray(z, f32)
+    z = np.asarray(z, dt)
     mx = z.max(-1, keepdims=True)
-    lse = mx + np.log(np.exp(z - mx).sum(-1, keepdims=True, dtype=f32)).astype(f32)
-    return (z - lse).astype(f32)
+    lse = mx + np.log(np.exp(z - mx).sum(-1, keepdims=True, dtype=dt)).astype(dt)
+    return (z - lse).astype(dt)
 
 
-def categorical_logp_entropy(logits, actions):
+def categorical_logp_entropy(logits, actions, dt=f32):
     """log_prob (categorical.py:156) and entropy with log p clamped at finfo.min (:158-162)."""
-    lp = log_softmax(logits)
+    lp = log_softmax(logits, dt)
     p = np.exp(lp)
     logp = np.take_along_axis(lp, np.asarray(actions, np.int64)[..., None], -1)[..., 0]
-    lpc = np.maximum(lp, np.finfo(np.float32).min)
+    lpc = np.maximum(lp, np.finfo(dt).min)
     ent = -(lpc * p).sum(-1)
-    return logp.astype(f32), ent.astype(f32), p, lp
+    return logp.astype(dt), ent.astype(dt), p, lp
 
 
 LOG_SQRT_2PI = math.log(math.sqrt(2 * math.pi))
 
 
-def normal_logp_entropy(mean, log_std, actions):
+def normal_logp_entropy(mean, log_std, actions, dt=f32):
     """JointNormal (continuous_ppo.py:40-47) over torch Normal (distributions/normal.py:88-116):
     log_prob = sum_a [-(x-mu)^2/(2 sigma^2) - log sigma - log sqrt(2 pi)],
     entropy  = sum_a [0.5 + 0.5 log(2 pi) + log sigma], sigma = exp(log_std)."""
-    sigma = np.exp(np.asarray(log_std, f32))
+    sigma = np.exp(np.asarray(log_std, dt))
     var = sigma * sigma
     log_scale = np.log(sigma)
-    x = np.asarray(actions, f32)
-    lp = (-((x - mean) ** 2) / (2 * var) - log_scale - f32(LOG_SQRT_2PI)).sum(-1)
-    ent = np.broadcast_to(f32(0.5 + 0.5 * math.log(2 * math.pi)) + log_scale, mean.shape).sum(-1)
-    return lp.astype(f32), ent.astype(f32)
+    x = np.asarray(actions, dt)
+    lp = (-((x - mean) ** 2) / (2 * var) - log_scale - dt(LOG_SQRT_2PI)).sum(-1)
+    ent = np.broadcast_to(dt(0.5 + 0.5 * math.log(2 * math.pi)) + log_scale, mean.shape).sum(-1)
+    return lp.astype(dt), ent.astype(dt)
 
 
 def old_policy(params, obs, actions, next_obs, continuous=False):
@@ -172,17 +172,22 @@ def old_policy(params, obs, actions, next_obs, continuous=False):
 # Loss + analytic backward for one minibatch (ppo.py:261-283; continuous_ppo.py:273-295)
 # ---------------------------------------------------------------------------------------------
 def minibatch_loss_grads(params, obs, actions, old_logp, adv, ret, hp: Hyper, continuous=False,
-                         m_total=None):
+                         m_total=None, dt=f32):
     """Returns (loss, components, grads).  ``m_total`` is the size the means divide by
-    (the global minibatch size; equals len(obs) on one device)."""
+    (the global minibatch size; equals len(obs) on one device).  ``dt=np.float64`` evaluates the
+    same formulas in double precision: the exact-math yardstick the parity tests measure both
+    float32 implementations against at full minibatch sizes (65,536-131,072-term sums)."""
     m = obs.shape[0] if m_total is None else m_total
+    f32 = dt  # noqa: N806 -- every float32 cast below follows the requested precision
+    if dt is not np.float32:
+        params = {k: np.asarray(v, dt) for k, v in params.items()}
     head = "actor_mean_head" if continuous else "actor_head"
-    f = forward(params, obs, continuous)
+    f = forward(params, obs, continuous, dt)
     eps = f32(hp.ppo_clip)
     if continuous:
-        logp, ent = normal_logp_entropy(f["out"], params["actor_log_std"], actions)
+        logp, ent = normal_logp_entropy(f["out"], params["actor_log_std"], actions, dt)
     else:
-        logp, ent, p, lp = categorical_logp_entropy(f["out"], actions)
+        logp, ent, p, lp = categorical_logp_entropy(f["out"], actions, dt)
     adv = np.asarray(adv, f32)
     ret = np.asarray(ret, f32)
     ratio = np.exp(logp - np.asarray(old_logp, f32))                       # ppo.py:266

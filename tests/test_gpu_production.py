@@ -1,0 +1,298 @@
+"""GPU parity of the minibatch kernel in its PRODUCTION configuration.
+
+``mb_kernel`` (csrc/mbstep.hip) launches G = min(ceil(m/32), 256) workgroups; each runs
+nit = ceil(ceil(m/32)/G) 32-sample steps through a two-team software pipeline (the forward team on
+step it while the backward team back-propagates step it-1, hand-off images double-buffered by step
+parity).  The golden-trace tests have minibatches of at most 4,096 samples, i.e. nit == 1: only
+one team is ever busy per interval set and the odd-parity buffers are never read.  Every BASELINE
+configuration runs nit = 8 (C2, C4) or 16 (C3).  These tests run those shapes:
+
+* one minibatch gradient at the full C2 / C3 / C4 minibatch sizes (65,536 / 131,072 / 65,536
+  samples, nit = 8 / 16 / 8), plus a ragged one (m % 32 != 0, workgroups with unequal step
+  counts), through ``dppo_minibatch_grad_f32`` against the oracle's ``minibatch_loss_grads`` on the
+  same sample records and indices (reference ppo.py:261-283, continuous_ppo.py:273-295);
+* a full ``learn()`` at intermediate sizes (nit = 2 and 3, discrete and continuous) and at the full
+  C2 size (nit = 8) against the oracle's ``learn`` with the same NumPy permutations
+  (ppo.py:224-287).
+
+Tolerances.  At these sizes every gradient entry is a sum of 65,536-131,072 fp32 terms, so BOTH
+fp32 implementations (the kernel and the NumPy oracle) carry a summation error of order
+eps32 * sqrt(m) relative to max|g| (~1.5e-5 at m = 65,536).  The yardstick is therefore the same
+oracle evaluated in float64 (``dt=np.float64``): the kernel must be within 2e-5 * max|g| of it
+per entry -- the small-size golden-trace bound -- and no further from it than 4x the fp32
+oracle's own distance (+1e-6 * max|g|).  Full learn(): losses / grad norms rel 1e-4 and
+parameters 2e-5 abs after 32 Adam steps against the fp32 oracle (test_learn_large_vs_oracle's
+bounds).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import diamond
+from diamond import _native as N
+from diamond.engine import DeviceRollout
+from oracle import ppo_np as P
+
+H = 64
+
+
+def dev():
+    return torch.device("cuda", 0)
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+class Box:
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+
+class Discrete:
+    def __init__(self, n):
+        self.n = int(n)
+
+
+class SpecEnvs:
+    """Spaces only: learn() on staged buffers never steps an environment."""
+
+    def __init__(self, D, A, cont):
+        self.single_observation_space = Box((D,))
+        self.single_action_space = Box((A,)) if cont else Discrete(A)
+
+
+def synth(T, Nn, D, A, cont, seed):
+    rng = np.random.default_rng(seed)
+    obs = rng.standard_normal((T, Nn, D), dtype=np.float32)
+    nobs = rng.standard_normal((T, Nn, D), dtype=np.float32)
+    act = (rng.standard_normal((T, Nn, A), dtype=np.float32) if cont
+           else rng.integers(0, A, (T, Nn)).astype(np.int32))
+    rew = rng.normal(1.0, 1.0, (T, Nn)).astype(np.float32)
+    te = (rng.random((T, Nn)) < (0.0 if cont else 0.02)).astype(np.uint8)
+    tr = (rng.random((T, Nn)) < (0.001 if cont else 0.005)).astype(np.uint8)
+    g = lambda x: torch.from_numpy(x).to(dev())
+    return DeviceRollout(g(obs), g(nobs), g(act), g(rew), g(te), g(tr)), (obs, nobs, act, rew, te, tr)
+
+
+def random_params(L, names, D, A, cont, rng):
+    """Parameters of the default network at a scale that keeps tanh units in their active range
+    and the policy away from uniform (so the surrogate's clip and both tie branches occur)."""
+    params = {}
+    for i, n in enumerate(names):
+        shp = (L.rows[i],) if n.endswith("bias") else (L.rows[i], L.cols[i])
+        if n == "actor_log_std":
+            params[n] = rng.normal(-0.5, 0.2, (1, A)).astype(np.float32)
+        elif n.endswith("bias"):
+            params[n] = rng.normal(0.0, 0.1, shp).astype(np.float32)
+        else:
+            params[n] = (rng.standard_normal(shp) * 1.2 / np.sqrt(shp[1])).astype(np.float32)
+    flat = np.zeros(L.total, np.float32)
+    for i, n in enumerate(names):
+        flat[L.offset[i]:L.offset[i] + L.numel[i]] = params[n].ravel()
+    return params, flat
+
+
+def hparams():
+    return N.HParams(gamma=0.99, gae_lambda=0.95, ppo_clip=0.2, value_loss_weight=1.0,
+                     entropy_beta=0.01, grad_norm_clip=0.5, adam_beta1=0.9, adam_beta2=0.999,
+                     adam_eps=1e-5, advantage_norm=1, lr=3e-4, adam_step=0)
+
+
+def nit_of(m):
+    steps = (m + 31) // 32
+    G = min(steps, 256)
+    return (steps + G - 1) // G
+
+
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,T,Nn,D,A,cont,ragged", [
+    ("C2 cartpole", 128, 4096, 4, 2, False, 0),
+    ("C3 lunar", 128, 8192, 8, 4, False, 0),
+    ("C4 cheetah", 128, 4096, 17, 6, True, 0),
+    ("C2 ragged", 128, 4096, 4, 2, False, 77),
+    ("C4 ragged", 128, 4096, 17, 6, True, 4093),
+])
+def test_full_minibatch_gradient_vs_oracle(name, T, Nn, D, A, cont, ragged):
+    E, M = 4, 8
+    B = T * Nn
+    h = N.Handle(0, N.Dims(T, Nn, D, A, int(cont), H, E, M, 1, 0))
+    L = h.layout
+    names = P.CONTINUOUS_NAMES if cont else P.DISCRETE_NAMES
+    rng = np.random.default_rng(B + D)
+    params, flat = random_params(L, names, D, A, cont, rng)
+    ro, host = synth(T, Nn, D, A, cont, seed=D * 7 + A)
+    pd = torch.from_numpy(flat).to(dev())
+    outs = {k: torch.empty(B, device=dev()) for k in
+            ("log_probs", "values", "next_values", "advantages", "returns")}
+    lo = N.LearnOutputs(*[outs[k].data_ptr() for k in
+                          ("log_probs", "values", "next_values", "advantages", "returns")])
+    hp = hparams()
+    N.check(h.lib.dppo_prepare_f32(h.h, ctypes.byref(ro.as_struct()), pd.data_ptr(),
+                                   ctypes.byref(hp), ctypes.byref(lo), stream()))
+    mb = B // M - ragged
+    assert nit_of(mb) >= 8
+    idx = np.random.RandomState(B).permutation(B)[:mb].astype(np.int32)
+    idx_d = torch.from_numpy(idx).to(dev())
+    g = torch.zeros(L.total, device=dev())
+    loss4 = (ctypes.c_float * 4)()
+    N.check(h.lib.dppo_minibatch_grad_f32(h.h, pd.data_ptr(), idx_d.data_ptr(), mb, mb,
+                                          ctypes.byref(hp), g.data_ptr(), loss4, stream()))
+    torch.cuda.synchronize()
+    got_flat = g.cpu().numpy()
+    got = np.concatenate([got_flat[L.offset[i]:L.offset[i] + L.numel[i]] for i in range(L.count)])
+    o = {k: v.cpu().numpy() for k, v in outs.items()}
+    obs, _, act, *_ = host
+    obs_f = obs.reshape(B, D)
+    act_f = act.reshape(B, A) if cont else act.reshape(B)
+    args = (obs_f[idx], act_f[idx], o["log_probs"][idx], o["advantages"][idx], o["returns"][idx])
+    res = {}
+    for dt in (np.float32, np.float64):
+        loss, comps, grads = P.minibatch_loss_grads(params, *args, P.Hyper(), cont, dt=dt)
+        res[dt] = (loss, comps, np.concatenate([np.asarray(grads[n], np.float64).ravel()
+                                                for n in names]))
+    exact = res[np.float64][2]
+    scale = np.abs(exact).max()
+    err_kernel = np.abs(got - exact).max() / scale
+    err_oracle32 = np.abs(res[np.float32][2] - exact).max() / scale
+    assert err_kernel <= 2e-5, (name, err_kernel, err_oracle32)
+    assert err_kernel <= 4 * err_oracle32 + 1e-6, (name, err_kernel, err_oracle32)
+    # per tensor, relative to the tensor's own scale (small tensors are not hidden by big ones)
+    for i, n in enumerate(names):
+        a = got[sum(L.numel[k] for k in range(i)):][:L.numel[i]]
+        b = exact[sum(L.numel[k] for k in range(i)):][:L.numel[i]]
+        s = max(np.abs(b).max(), 1e-3 * scale)
+        assert np.abs(a - b).max() <= 1e-4 * s, (name, n, np.abs(a - b).max() / s)
+    loss, comps, _ = res[np.float64]
+    assert abs(loss4[0] - loss) <= 2e-5 * max(1.0, abs(loss)), (loss4[0], loss)
+    assert abs(loss4[1] - comps["loss_policy"]) <= 2e-5 * max(1.0, abs(comps["loss_policy"]))
+    assert abs(loss4[2] - comps["loss_value"]) <= 2e-5 * max(1.0, abs(comps["loss_value"]))
+    assert abs(loss4[3] - comps["entropy"]) <= 2e-5 * max(1.0, abs(comps["entropy"]))
+
+
+@pytest.mark.parametrize("name,T,Nn,D,A,cont", [
+    ("C3 lunar eval", 128, 8192, 8, 4, False),
+    ("C4 cheetah eval", 128, 4096, 17, 6, True),
+])
+def test_full_size_old_policy_and_records_vs_oracle(name, T, Nn, D, A, cont):
+    """prepare() at full BASELINE sizes: old-policy log-probs / values / next-values (eval_kernel)
+    against the oracle's old_policy, advantages bit-exact through GAE, normalisation rel 2e-6."""
+    E, M = 4, 8
+    B = T * Nn
+    h = N.Handle(0, N.Dims(T, Nn, D, A, int(cont), H, E, M, 1, 0))
+    L = h.layout
+    names = P.CONTINUOUS_NAMES if cont else P.DISCRETE_NAMES
+    params, flat = random_params(L, names, D, A, cont, np.random.default_rng(3))
+    ro, host = synth(T, Nn, D, A, cont, seed=11)
+    pd = torch.from_numpy(flat).to(dev())
+    outs = {k: torch.empty(B, device=dev()) for k in
+            ("log_probs", "values", "next_values", "advantages", "returns")}
+    lo = N.LearnOutputs(*[outs[k].data_ptr() for k in
+                          ("log_probs", "values", "next_values", "advantages", "returns")])
+    hp = hparams()
+    N.check(h.lib.dppo_prepare_f32(h.h, ctypes.byref(ro.as_struct()), pd.data_ptr(),
+                                   ctypes.byref(hp), ctypes.byref(lo), stream()))
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in outs.items()}
+    obs, nobs, act, rew, te, tr = host
+    logp, v, nv, _ = P.old_policy(params, obs, act, nobs, cont)
+    np.testing.assert_allclose(o["log_probs"], logp.ravel(), rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(o["values"], v.ravel(), rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(o["next_values"], nv.ravel(), rtol=2e-5, atol=2e-5)
+    # GAE on the kernel's own values is bit-exact; the stored returns are values + raw advantages
+    vals = o["values"].reshape(T, Nn)
+    adv = P.gae(rew, te, tr, vals, o["next_values"].reshape(T, Nn))
+    assert np.array_equal(o["returns"].reshape(T, Nn), vals + adv)
+    np.testing.assert_allclose(o["advantages"], P.normalize_adv(adv).ravel(), rtol=0, atol=2e-6)
+
+
+# ---------------------------------------------------------------------------------------------
+def learn_vs_oracle(T, Nn, D, A, cont, seed):
+    Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
+    Agent = diamond.ContinuousPPO if cont else diamond.PPO
+    cfg = Cfg(rollout_steps=T, num_envs=Nn, verbose=False)
+    agent = Agent(None, cfg, envs=SpecEnvs(D, A, cont))
+    assert agent._learner.fused
+    mb = T * Nn // cfg.num_minibatches
+    names = [n for n, _ in agent.network.named_parameters()]
+    params = {n: p.detach().cpu().numpy().copy() for n, p in agent.network.named_parameters()}
+    ro, host = synth(T, Nn, D, A, cont, seed)
+    np.random.seed(seed)
+    st = np.random.get_state()
+    agent.learn_device(ro)
+    tr = agent.learn_trace()
+    torch.cuda.synchronize()
+    np.random.set_state(st)
+    adam = P.new_adam_state(params, names)
+    ref = P.learn(params, adam, list(host), P.Hyper(), cfg.lr, cont, rng=np.random)
+    np.testing.assert_allclose(tr[:, 0], ref["loss"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(tr[:, 4], ref["norm"], rtol=1e-4, atol=1e-5)
+    for n, p in agent.network.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), params[n], rtol=0, atol=2e-5,
+                                   err_msg=n)
+    return mb
+
+
+@pytest.mark.parametrize("T,Nn,D,A,cont,want_nit", [
+    (128, 1024, 4, 2, False, 2),     # mb 16,384: every workgroup two steps
+    (128, 1536, 8, 4, False, 3),     # mb 24,576: three steps
+    (128, 768, 17, 6, True, 2),      # mb 12,288: 384 steps over 256 workgroups (ragged nit)
+    (100, 1000, 5, 3, False, 2),     # mb 12,500: 391 steps, the last one partial
+])
+def test_learn_intermediate_nit_vs_oracle(T, Nn, D, A, cont, want_nit):
+    mb = learn_vs_oracle(T, Nn, D, A, cont, seed=T + Nn)
+    assert nit_of(mb) == want_nit
+
+
+def test_learn_full_c2_vs_oracle():
+    """BASELINE configs[1] itself: CartPole PPO, T = 128, N = 4096 (mb 65,536, nit = 8)."""
+    mb = learn_vs_oracle(128, 4096, 4, 2, False, seed=0)
+    assert nit_of(mb) == 8
+
+
+# ---------------------------------------------------------------------------------------------
+def test_grid_fanin_reports_non_resident_grid():
+    """The single-device optimizer step (reduce_adam_kernel, and the optional fused tail of the
+    minibatch kernel) meets in a grid-wide fan-in.  Its wait is bounded: a grid that cannot be
+    co-resident drains after the timeout and raises the handle's sticky error, which every later
+    call reports (DPPO_EHIP -> RuntimeError) -- an error return, not numbers from stale partials."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    T, Nn, D, A = 16, 64, 4, 2
+    h = N.Handle(0, N.Dims(T, Nn, D, A, 0, H, 4, 8, 1, 0))
+    lib = h.lib
+    # resident: one 1024-thread workgroup per CU (96 KB of LDS each: two never share a CU)
+    N.check(lib.dppo_fanin_selftest(h.h, cus, 96 * 1024, 2_000_000, stream()))
+    torch.cuda.synchronize()
+    assert lib.dppo_status(h.h) == N.DPPO_OK
+    # a learn on the same handle still works and moves the parameters
+    L = h.layout
+    names = P.DISCRETE_NAMES
+    params, flat = random_params(L, names, D, A, False, np.random.default_rng(0))
+    ro, _ = synth(T, Nn, D, A, False, seed=1)
+    pd = torch.from_numpy(flat).to(dev())
+    m = torch.zeros_like(pd)
+    v = torch.zeros_like(pd)
+    perms = np.stack([np.random.RandomState(e).permutation(T * Nn) for e in range(4)]).astype(np.int32)
+    hp = hparams()
+    st = ro.as_struct()
+    N.check(lib.dppo_learn_f32(h.h, ctypes.byref(st), pd.data_ptr(), m.data_ptr(), v.data_ptr(),
+                               ctypes.byref(hp), perms.ctypes.data, None, stream()))
+    torch.cuda.synchronize()
+    after_ok = pd.cpu().numpy()
+    assert not np.array_equal(after_ok, flat)
+    # NOT co-resident: 8 more workgroups than CUs, each needing a CU of its own
+    N.check(lib.dppo_fanin_selftest(h.h, cus + 8, 96 * 1024, 20_000, stream()))
+    torch.cuda.synchronize()
+    assert lib.dppo_status(h.h) == N.DPPO_EHIP
+    assert b"fan-in timed out" in lib.dppo_last_error()
+    rc = lib.dppo_learn_f32(h.h, ctypes.byref(st), pd.data_ptr(), m.data_ptr(), v.data_ptr(),
+                            ctypes.byref(hp), perms.ctypes.data, None, stream())
+    assert rc == N.DPPO_EHIP
+    torch.cuda.synchronize()
+    assert np.array_equal(pd.cpu().numpy(), after_ok)   # nothing was enqueued
+    with pytest.raises(N.NativeError):
+        h.trace(32)
