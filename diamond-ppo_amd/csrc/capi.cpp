@@ -68,6 +68,9 @@ struct LoopGroup {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
+  // set when a barrier timed out or a member was destroyed: every member's exchange then fails
+  // with DPPO_ECOMM (arrival counts and peer buffers can no longer be trusted)
+  bool broken = false;
   dppo_handle* members[kMaxLoopRanks] = {};
   void* bufs[kMaxLoopRanks] = {};
 };
@@ -90,6 +93,15 @@ struct dppo_handle {
   bool mlp_ok = false;
   int64_t B = 0;   // local samples T*N
   int32_t mb = 0;  // local minibatch size B / M
+  // global-minibatch data parallelism (dims.global_minibatches with world_size > 1): the host
+  // permutations cover the global batch Bg = B * world; shard_select turns them into this rank's
+  // per-epoch local lists + minibatch boundaries
+  bool gmb = false;
+  int64_t Bg = 0;
+  int64_t pe = 0;                    // permutation entries per epoch: Bg (global) or B (local)
+  int32_t* perms_local = nullptr;    // [E][B]
+  int32_t* seg = nullptr;            // [E][M + 1]
+  int32_t* sel_cnt = nullptr;        // [E][shard_select_chunks(Bg)]
   int G = 1;       // workgroups (= gradient slabs) of the fused minibatch kernel
   int num_cus = 256;
   int64_t slab_stride = 0;
@@ -311,6 +323,10 @@ inline int world_of(const dppo_handle* h) { return distributed(h) ? h->nranks : 
 
 int loop_barrier(LoopGroup* g) {
   std::unique_lock<std::mutex> lk(g->mu);
+  if (g->broken) {
+    set_error("loopback group is broken (an earlier exchange timed out or a member was destroyed)");
+    return DPPO_ECOMM;
+  }
   const uint64_t gen = g->gen;
   if (++g->arrived == g->n) {
     g->arrived = 0;
@@ -318,8 +334,15 @@ int loop_barrier(LoopGroup* g) {
     g->cv.notify_all();
     return DPPO_OK;
   }
-  if (!g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->gen != gen; })) {
+  if (!g->cv.wait_for(lk, std::chrono::seconds(120),
+                      [&] { return g->gen != gen || g->broken; })) {
+    g->broken = true;
+    g->cv.notify_all();
     set_error("loopback group: a rank did not reach the all-reduce within 120 s");
+    return DPPO_ECOMM;
+  }
+  if (g->gen == gen) {  // woken by a break, not by the last arriver
+    set_error("loopback group is broken (an exchange timed out or a member was destroyed)");
     return DPPO_ECOMM;
   }
   return DPPO_OK;
@@ -333,19 +356,22 @@ int loop_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s)
               h->loop_bytes);
     return DPPO_EINVAL;
   }
+  // The peers' readiness is awaited on the HOST (hipEventSynchronize), never by a device-side
+  // wait on another rank's stream: with more ranks than hardware queues (GPU_MAX_HW_QUEUES)
+  // streams share queues, and a cross-stream barrier packet could then wait on work queued behind
+  // it.  Test-only path: two host synchronisations per exchange are fine.
   g->bufs[h->rank] = buf;
   DPPO_HIP_CHECK(hipEventRecord(h->loop_ready, s));
   DPPO_TRY(loop_barrier(g));
   RankPtrs src{};
   for (int r = 0; r < g->n; ++r) {
     src.p[r] = g->bufs[r];
-    if (r != h->rank) DPPO_HIP_CHECK(hipStreamWaitEvent(s, g->members[r]->loop_ready, 0));
+    DPPO_HIP_CHECK(hipEventSynchronize(g->members[r]->loop_ready));
   }
   DPPO_TRY(launch_rank_sum(src, g->n, h->loop_out, (int64_t)n, f64, s));
   DPPO_HIP_CHECK(hipEventRecord(h->loop_done, s));
   DPPO_TRY(loop_barrier(g));
-  for (int r = 0; r < g->n; ++r)
-    if (r != h->rank) DPPO_HIP_CHECK(hipStreamWaitEvent(s, g->members[r]->loop_done, 0));
+  for (int r = 0; r < g->n; ++r) DPPO_HIP_CHECK(hipEventSynchronize(g->members[r]->loop_done));
   DPPO_HIP_CHECK(hipMemcpyAsync(buf, h->loop_out, bytes, hipMemcpyDeviceToDevice, s));
   return DPPO_OK;
 }
@@ -430,13 +456,14 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
 }
 
 // One minibatch: fused gradient kernel -> slab reduction -> [all-reduce] (grad left in h->grad).
-int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int32_t m,
-                   int32_t m_total, const dppo_hparams* hp, hipStream_t s) {
+int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, const int32_t* seg,
+                   int32_t m, int32_t m_total, const dppo_hparams* hp, hipStream_t s) {
   const dppo_dims& d = h->dims;
   GradArgs ga{};
   ga.params = params;
   ga.rec = h->rec;
   ga.idx = idx;
+  ga.seg = seg;
   ga.m = m;
   ga.inv_m = (float)(1.0 / (double)m_total);
   ga.clip_eps = hp->ppo_clip;
@@ -445,7 +472,9 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, int3
   ga.slabs = h->slabs;
   ga.slab_stride = h->slab_stride;
   ga.p_total = h->layout.total;
-  int G = mb_grid(m);
+  // with `seg` the size is known only on the device: the handle's grid (sized for the largest
+  // share a rank can hold) -- workgroups past the last step contribute zero slabs
+  int G = seg ? h->G : mb_grid(m);
   if (G > h->G) G = h->G;
   {
     Timed tm(h, K_GRAD, s);
@@ -475,7 +504,7 @@ namespace {
 // and the launch stream waits on it before the first kernel that reads the permutations.  A
 // pinned slot is copied from directly (pure DMA); any other buffer is first staged in slot 0.
 int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, int ds) {
-  const size_t pbytes = (size_t)(h->dims.num_epochs * h->B) * sizeof(int32_t);
+  const size_t pbytes = (size_t)(h->dims.num_epochs * h->pe) * sizeof(int32_t);
   int slot = host == h->perms_pinned[1] ? 1 : 0;
   if (host != h->perms_pinned[slot]) {
     if (h->perm_copy_pending[0]) DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done[0]));
@@ -500,11 +529,16 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
   }
   DPPO_TRY(device_status(h));
   const dppo_dims& d = h->dims;
-  if (h->B % d.num_minibatches != 0) {
+  if (h->pe % d.num_minibatches != 0) {
     // the reference's perms.reshape(E, M, B // M) raises ValueError (ppo.py:255)
     set_error("cannot reshape array of size %lld into shape (%d,%d,%lld)",
-              (long long)(h->B * d.num_epochs), d.num_epochs, d.num_minibatches,
-              (long long)(h->B / d.num_minibatches));
+              (long long)(h->pe * d.num_epochs), d.num_epochs, d.num_minibatches,
+              (long long)(h->pe / d.num_minibatches));
+    return DPPO_EINVAL;
+  }
+  if (h->gmb && !(distributed(h) && h->nranks == d.world_size)) {
+    set_error("global_minibatches needs the world_size=%d communicator (dppo_comm_init or "
+              "dppo_loopback_group) before dppo_learn_f32", d.world_size);
     return DPPO_EINVAL;
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
@@ -520,17 +554,27 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
   DPPO_HIP_CHECK(hipStreamWaitEvent(s, h->perms_ready, 0));
   if (targets) {
     Timed tm(h, K_PERM, s);
-    DPPO_TRY(launch_perm_resolve(h->targets_dev2[ds], h->perms_dev, h->B, (int32_t)E,
+    DPPO_TRY(launch_perm_resolve(h->targets_dev2[ds], h->perms_dev, h->pe, (int32_t)E,
                                  h->perm_scratch, s));
+  }
+  if (h->gmb) {
+    // this rank's members of every global minibatch, in permutation order
+    Timed tm(h, K_PERM, s);
+    DPPO_TRY(launch_shard_select(h->perms_dev, h->perms_local, h->seg, h->sel_cnt, h->Bg,
+                                 d.num_envs * h->nranks, d.num_envs * h->rank, d.num_envs,
+                                 (int32_t)E, (int32_t)M, s));
   }
   // (6) E x M dependent optimizer steps (ppo.py:258-285)
   const int32_t mb = h->mb;
-  const int32_t m_total = mb * world_of(h);
+  // global minibatch size: the divisor of every mean (ppo.py:270-274)
+  const int32_t m_total = h->gmb ? (int32_t)(h->Bg / M) : mb * world_of(h);
   const float inv_m = (float)(1.0 / (double)m_total);
   for (int64_t e = 0; e < E; ++e) {
     for (int64_t j = 0; j < M; ++j) {
       const int64_t k = e * M + j;
-      const int32_t* idx = h->perms_dev + e * h->B + j * mb;
+      const int32_t* idx =
+          h->gmb ? h->perms_local + e * h->B : h->perms_dev + e * h->B + j * mb;
+      const int32_t* seg = h->gmb ? h->seg + e * (M + 1) + j : nullptr;
       const double step = (double)(hp->adam_step + k + 1);
       const double bc1 = 1.0 - std::pow((double)hp->adam_beta1, step);
       const double bc2 = 1.0 - std::pow((double)hp->adam_beta2, step);
@@ -608,7 +652,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
             hp->entropy_beta, h->err_dev, h->fanin_ticks, s));
         continue;
       }
-      DPPO_TRY(minibatch_grad(h, params, idx, mb, m_total, hp, s));
+      DPPO_TRY(minibatch_grad(h, params, idx, seg, mb, m_total, hp, s));
       Timed tm(h, K_ADAM, s);
       // after the all-reduce the reduce kernel's per-block norm partials are stale: the Adam
       // kernel recomputes the norm from the gradient itself
@@ -660,6 +704,9 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   h->mb = (int32_t)(h->B / dims->num_minibatches);
   h->rank = dims->rank;
   h->nranks = dims->world_size;
+  h->gmb = dims->global_minibatches != 0 && dims->world_size > 1;
+  h->Bg = h->B * dims->world_size;
+  h->pe = h->gmb ? h->Bg : h->B;
   const int D8 = (dims->obs_dim + 7) / 8 * 8;
   h->sh.D = dims->obs_dim;
   h->sh.D8 = D8;
@@ -676,7 +723,9 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
       cus <= 0)
     cus = 256;
   h->num_cus = cus;
-  h->G = mb_grid(h->mb > 0 ? h->mb : 1);
+  // global minibatches: a rank's share of one varies around mb; size the grid for a whole one
+  h->G = mb_grid(h->gmb ? (int32_t)std::min<int64_t>(h->Bg / dims->num_minibatches, h->B)
+                        : (h->mb > 0 ? h->mb : 1));
   if (h->G > cus) h->G = cus;
   h->slab_stride = round_up(h->layout.total + 8, 64);
   const int64_t E = dims->num_epochs, M = dims->num_minibatches;
@@ -701,11 +750,16 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
   chk(dalloc(&h->arrivals, 4 * kArrivalWords));
   for (int k = 0; k < 2; ++k) {
-    chk(dalloc(&h->perms_dev2[k], E * h->B));
-    chk(dalloc(&h->targets_dev2[k], E * h->B));
+    chk(dalloc(&h->perms_dev2[k], E * h->pe));
+    chk(dalloc(&h->targets_dev2[k], E * h->pe));
   }
   h->perms_dev = h->perms_dev2[0];
-  chk(dalloc(&h->perm_scratch, 3 * E * h->B));
+  chk(dalloc(&h->perm_scratch, 3 * E * h->pe));
+  if (h->gmb) {
+    chk(dalloc(&h->perms_local, E * h->B));
+    chk(dalloc(&h->seg, E * (M + 1)));
+    chk(dalloc(&h->sel_cnt, E * shard_select_chunks(h->Bg)));
+  }
   if (rc == DPPO_OK) {
     if (hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->perms_ready, hipEventDisableTiming) != hipSuccess ||
@@ -731,7 +785,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   h->radam_ok = reduce_adam_capacity(device) >= reduce_adam_blocks(h->layout.total);
   for (int k = 0; k < 2 && rc == DPPO_OK; ++k) {
     hipError_t e = hipHostMalloc((void**)&h->perms_pinned[k],
-                                 (size_t)(E * h->B) * sizeof(int32_t), hipHostMallocDefault);
+                                 (size_t)(E * h->pe) * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
       set_error("hipHostMalloc failed: %s", hipGetErrorString(e));
       rc = DPPO_ENOMEM;
@@ -760,6 +814,13 @@ void dppo_destroy(dppo_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   (void)hipDeviceSynchronize();
+  if (h->loop) {  // peers must never touch this handle's events or buffers again
+    std::lock_guard<std::mutex> lk(h->loop->mu);
+    h->loop->broken = true;
+    h->loop->members[h->rank] = nullptr;
+    h->loop->bufs[h->rank] = nullptr;
+    h->loop->cv.notify_all();
+  }
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->loop_out) (void)hipFree(h->loop_out);
   if (h->loop_ready) (void)hipEventDestroy(h->loop_ready);
@@ -787,6 +848,9 @@ void dppo_destroy(dppo_handle* h) {
   if (h->perms_ready) (void)hipEventDestroy(h->perms_ready);
   if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   (void)hipFree(h->perm_scratch);
+  (void)hipFree(h->perms_local);
+  (void)hipFree(h->seg);
+  (void)hipFree(h->sel_cnt);
   for (int k = 0; k < 2; ++k) {
     if (h->perms_pinned[k]) (void)hipHostFree(h->perms_pinned[k]);
     if (h->perm_copy_done[k]) (void)hipEventDestroy(h->perm_copy_done[k]);
@@ -901,7 +965,7 @@ int dppo_minibatch_grad_f32(dppo_handle* h, const float* params, const int32_t* 
   DPPO_TRY(require_mlp(h));
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t s = S(stream);
-  DPPO_TRY(minibatch_grad(h, params, idx, m, m_total, hp, s));
+  DPPO_TRY(minibatch_grad(h, params, idx, nullptr, m, m_total, hp, s));
   DPPO_HIP_CHECK(hipMemcpyAsync(grad, h->grad, (size_t)h->layout.total * sizeof(float),
                                 hipMemcpyDeviceToDevice, s));
   if (loss4) {
@@ -1033,6 +1097,15 @@ int dppo_comm_unique_id(char* out128) {
 int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128) {
   if (!h || !id128 || nranks < 1 || rank < 0 || rank >= nranks) {
     set_error("invalid argument to dppo_comm_init");
+    return DPPO_EINVAL;
+  }
+  if (h->comm || h->loop) {
+    set_error("dppo_comm_init: the handle already has a communicator or loopback group");
+    return DPPO_EINVAL;
+  }
+  if (h->gmb && nranks != h->dims.world_size) {
+    set_error("dppo_comm_init: global_minibatches handle of world_size %d cannot join %d ranks",
+              h->dims.world_size, nranks);
     return DPPO_EINVAL;
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));

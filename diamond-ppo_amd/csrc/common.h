@@ -197,7 +197,8 @@ struct GradArgs {
   const float* params;
   const float* rec;
   const int32_t* idx;  // minibatch sample indices (local)
-  int32_t m;           // samples in this minibatch on this rank
+  const int32_t* seg;  // or null; else device {start, end}: the minibatch is idx[start, end)
+  int32_t m;           // samples in this minibatch on this rank (ignored when seg is set)
   float inv_m;         // 1 / global minibatch size
   float clip_eps, vf_coef, ent_coef;
   float* slabs;        // [G][slab_stride]
@@ -269,5 +270,14 @@ int launch_rank_sum(const RankPtrs& src, int n, void* out, int64_t count, bool f
 // scratch = 3 * count * n int32.
 int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
                         int32_t* scratch, hipStream_t s);
+
+// Global-minibatch data parallelism (shuffle.hip): from E global permutations gperm[E][T*Ng]
+// keep, in order, the samples of env shard [env0, env0 + Nl) as local indices t*Nl + (n - env0)
+// into local[E][T*Nl]; seg[E][M+1] = where each global minibatch (mbg samples) starts in the
+// epoch's list.  cnt: scratch of E * shard_select_chunks(T*Ng) ints.
+int shard_select_chunks(int64_t bg);
+int launch_shard_select(const int32_t* gperm, int32_t* local, int32_t* seg, int32_t* cnt,
+                        int64_t bg, int32_t ng, int32_t env0, int32_t nl, int32_t E, int32_t M,
+                        hipStream_t s);
 
 }  // namespace dppo

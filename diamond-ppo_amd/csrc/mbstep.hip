@@ -108,6 +108,7 @@ struct MArgs {
   const float* params;
   const float* rec;
   const int32_t* idx;
+  const int32_t* seg;  // global-minibatch DP: {start, end} of this minibatch in idx (device)
   int m;
   float inv_m, clip_eps, vf, ent;
   float* slabs;
@@ -444,7 +445,15 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
   const int row0 = 16 * q;  // this wave's feature rows
   const int SX0 = L.SX0;
   const int nk1 = a.D16 / 4;  // layer-1 k-steps (4 or 8)
-  const int nsteps = (a.m + S - 1) / S;
+  // this rank's share of a global minibatch is known only on the device (shard_select, shuffle.hip)
+  int mm = a.m;
+  const int32_t* idxp = a.idx;
+  if (a.seg) {
+    const int s0 = a.seg[0];
+    mm = a.seg[1] - s0;
+    idxp += s0;
+  }
+  const int nsteps = (mm + S - 1) / S;
   const int nit = (nsteps + (int)gridDim.x - 1) / (int)gridDim.x;  // steps per workgroup
   float* slab = a.slabs + (int64_t)blockIdx.x * a.slab_stride;
 
@@ -521,12 +530,12 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     auto load_idx = [&](int it) {
       const int step = it * (int)gridDim.x + (int)blockIdx.x;
       const int si = step * S + hs;
-      nidx = (it < nit && si < a.m) ? a.idx[si] : 0;
+      nidx = (it < nit && si < mm) ? idxp[si] : 0;
     };
     auto load_rec = [&](int it) {
       const int step = it * (int)gridDim.x + (int)blockIdx.x;
       const int si = step * S + hs;
-      const bool valid = it < nit && si < a.m;
+      const bool valid = it < nit && si < mm;
       const float* rec = a.rec + (int64_t)nidx * a.R;
       pobs = (valid && hj < nk1 && 4 * hj < a.D8) ? *(const f32x4*)(rec + 4 * hj)
                                                  : (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -665,7 +674,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #endif
       if (act) {
         const int si = step * S + hs;
-        const bool valid = si < a.m;
+        const bool valid = si < mm;
         const f32x4 sc = csc;  // {action bits, old logp, adv, return}
         const float* hrow = HAC + hs * SAC;
         const f32x4 ha0 = *(const f32x4*)(hrow + 4 * hj), ha1 = *(const f32x4*)(hrow + 32 + 4 * hj);
@@ -1058,6 +1067,7 @@ int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, in
   k.params = ga.params;
   k.rec = ga.rec;
   k.idx = ga.idx;
+  k.seg = ga.seg;
   k.m = ga.m;
   k.inv_m = ga.inv_m;
   k.clip_eps = ga.clip_eps;

@@ -95,6 +95,97 @@ __global__ __launch_bounds__(kBlock) void fy_solve_kernel(const int32_t* __restr
   }
 }
 
+// ---- Global-minibatch data parallelism (dims.global_minibatches).
+// Every rank holds the SAME E permutations of the global batch (reference ppo.py:252-255 over
+// Bg = T*Ng samples, global flat index i = t*Ng + n).  Rank r keeps, in permutation order, the
+// members of each global minibatch whose env n is in its shard [env0, env0 + Nl), as local flat
+// indices t*Nl + (n - env0).  Per epoch the kept indices are a permutation of the rank's B = T*Nl
+// samples grouped by global minibatch; seg[e][j] is where minibatch j starts, seg[e][M] = B.
+// Two coalesced passes over the E*Bg ints, chunk-parallel over the whole chip:
+//   count : matches per 16,384-element chunk
+//   write : chunk start = sum of the epoch's earlier chunk counts; an ordered (ballot / mbcnt)
+//           compaction per 256-element slice; the thread holding position j*mbg records seg[e][j]
+constexpr int kSelPer = 64;                    // slices per chunk
+constexpr int kSelChunk = kBlock * kSelPer;    // 16,384 elements
+
+__device__ __forceinline__ bool in_shard(int32_t i, int32_t ng, int32_t env0, int32_t nl) {
+  const int32_t t = i / ng;
+  return (uint32_t)(i - t * ng - env0) < (uint32_t)nl;
+}
+
+__global__ __launch_bounds__(kBlock) void shard_count_kernel(const int32_t* __restrict__ gperm,
+                                                            int32_t* __restrict__ cnt, int64_t bg,
+                                                            int32_t ng, int32_t env0, int32_t nl) {
+  __shared__ int32_t wsum[kBlock / 64];
+  const int64_t e = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * kSelChunk;
+  const int32_t* src = gperm + e * bg;
+  int32_t k = 0;
+  for (int s = 0; s < kSelPer; ++s) {
+    const int64_t p = c0 + (int64_t)s * kBlock + threadIdx.x;
+    if (p < bg && in_shard(src[p], ng, env0, nl)) ++k;
+  }
+  for (int off = 32; off >= 1; off >>= 1) k += __shfl_xor(k, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += wsum[w];
+    cnt[e * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void shard_write_kernel(
+    const int32_t* __restrict__ gperm, const int32_t* __restrict__ cnt,
+    int32_t* __restrict__ local, int32_t* __restrict__ seg, int64_t bg, int32_t ng, int32_t env0,
+    int32_t nl, int32_t M) {
+  __shared__ int32_t red[kBlock / 64];
+  __shared__ int32_t wtot[2][kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t e = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * kSelChunk;
+  const int32_t* src = gperm + e * bg;
+  const int64_t B = (int64_t)(bg / ng) * nl;
+  const int64_t mbg = bg / M;
+  // start of this chunk in the epoch's local list
+  int32_t before = 0;
+  for (int c = threadIdx.x; c < (int)blockIdx.x; c += kBlock) before += cnt[e * gridDim.x + c];
+  for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off);
+  if (lane == 0) red[wave] = before;
+  __syncthreads();
+  int32_t base = 0;
+  for (int w = 0; w < kBlock / 64; ++w) base += red[w];
+  int32_t* out = local + e * B;
+  for (int s = 0; s < kSelPer; ++s) {
+    const int64_t p = c0 + (int64_t)s * kBlock + threadIdx.x;
+    int32_t i = 0;
+    bool keep = false;
+    if (p < bg) {
+      i = src[p];
+      keep = in_shard(i, ng, env0, nl);
+    }
+    const unsigned long long mask = __ballot(keep);
+    const int32_t pre = (int32_t)__builtin_amdgcn_mbcnt_hi(
+        (unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+    if (lane == 0) wtot[s & 1][wave] = (int32_t)__popcll(mask);
+    __syncthreads();
+    int32_t wpre = 0, tot = 0;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      const int32_t x = wtot[s & 1][w];
+      wpre += w < wave ? x : 0;
+      tot += x;
+    }
+    const int32_t pos = base + wpre + pre;  // kept samples before position p in this epoch
+    if (keep) {
+      const int32_t t = i / ng;
+      out[pos] = t * nl + (i - t * ng - env0);
+    }
+    if (p < bg && p % mbg == 0) seg[e * (M + 1) + p / mbg] = pos;
+    base += tot;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) seg[e * (M + 1) + M] = (int32_t)B;
+}
+
 int fy_grid(int64_t total) {
   int64_t b = (total + kBlock - 1) / kBlock;
   if (b > 8192) b = 8192;
@@ -117,6 +208,21 @@ int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32
   DPPO_LAUNCH(fy_links_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, mq, perms, n, total);
   DPPO_LAUNCH_CHECK();
   DPPO_LAUNCH(fy_solve_kernel, dim3(G), dim3(kBlock), 0, s, targets, mq, perms, n, total);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+int shard_select_chunks(int64_t bg) { return (int)((bg + kSelChunk - 1) / kSelChunk); }
+
+int launch_shard_select(const int32_t* gperm, int32_t* local, int32_t* seg, int32_t* cnt,
+                        int64_t bg, int32_t ng, int32_t env0, int32_t nl, int32_t E, int32_t M,
+                        hipStream_t s) {
+  if (bg <= 0 || E <= 0) return DPPO_OK;
+  const dim3 grid((unsigned)shard_select_chunks(bg), (unsigned)E);
+  DPPO_LAUNCH(shard_count_kernel, grid, dim3(kBlock), 0, s, gperm, cnt, bg, ng, env0, nl);
+  DPPO_LAUNCH_CHECK();
+  DPPO_LAUNCH(shard_write_kernel, grid, dim3(kBlock), 0, s, gperm, cnt, local, seg, bg, ng, env0,
+              nl, M);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

@@ -40,7 +40,8 @@ class Dims(ctypes.Structure):
                 ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32),
                 ("continuous", ctypes.c_int32), ("hidden", ctypes.c_int32),
                 ("num_epochs", ctypes.c_int32), ("num_minibatches", ctypes.c_int32),
-                ("world_size", ctypes.c_int32), ("rank", ctypes.c_int32)]
+                ("world_size", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("global_minibatches", ctypes.c_int32)]
 
 
 class HParams(ctypes.Structure):

@@ -51,6 +51,11 @@ class ContinuousPPOConfig:
     save_interval: float = 600
     verbose: bool = True
     device_index: int = 0
+    # data parallelism over ranks (additive): False = each rank permutes its own envs' samples and
+    # global minibatch j is the union of the ranks' local minibatches j; True = every rank draws
+    # the reference's permutations of the GLOBAL batch (ppo.py:252-255) and processes its members
+    # of each global minibatch, so N ranks reproduce the single-GPU learn() of the global batch
+    global_minibatches: bool = False
     tanh_squash: bool = False  # extension: env actions tanh(u), experience keeps u (module doc)
 
 

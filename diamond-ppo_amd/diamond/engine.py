@@ -291,11 +291,15 @@ class NativeLearner:
         self.world, self.rank = dist_world()
         self.T, self.N = cfg.rollout_steps, cfg.num_envs
         self.D, self.A = obs_dim, act_dim
+        # global minibatches (cfg.global_minibatches, world > 1): the permutations span the
+        # global batch of T * N * world samples and libdppo keeps this rank's members of each
+        self.global_mb = bool(getattr(cfg, "global_minibatches", False)) and self.world > 1
         self.dims = N.Dims(rollout_steps=self.T, num_envs=self.N, obs_dim=obs_dim,
                            act_dim=act_dim, continuous=int(continuous),
                            hidden=int(cfg.network_hidden_dim), num_epochs=cfg.num_epochs,
                            num_minibatches=cfg.num_minibatches, world_size=self.world,
-                           rank=self.rank)
+                           rank=self.rank, global_minibatches=int(self.global_mb))
+        self.perm_n = self.T * self.N * (self.world if self.global_mb else 1)
         self.handle = N.Handle(device.index or 0, self.dims)
         L = self.handle.layout
         names = [n for n, _ in network.named_parameters()]
@@ -380,7 +384,7 @@ class NativeLearner:
 
         def work():
             k = d["key_in"].copy()
-            d["pos_out"] = draw(k, d["pos_in"], self.T * self.N, self.cfg.num_epochs, buf)
+            d["pos_out"] = draw(k, d["pos_in"], self.perm_n, self.cfg.num_epochs, buf)
             d["key_out"] = k
             d["ok"] = True
 
@@ -404,13 +408,13 @@ class NativeLearner:
                 return d["buf"], d["key_out"], d["pos_out"]
         buf = self.handle.perm_buffer(self._slot)
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
-        pos = draw(key, pos, self.T * self.N, self.cfg.num_epochs, buf)
+        pos = draw(key, pos, self.perm_n, self.cfg.num_epochs, buf)
         N.set_mt_state(st, key, pos)
         return buf, key, pos
 
     def learn(self, ro: DeviceRollout, lr: float, outputs: N.LearnOutputs | None = None):
         cfg = self.cfg
-        B = self.T * self.N
+        B = self.perm_n
         if B % cfg.num_minibatches != 0:
             # reference: perms.reshape(E, M, B // M) raises (ppo.py:255)
             raise ValueError(f"cannot reshape array of size {B * cfg.num_epochs} into shape "
@@ -484,15 +488,39 @@ class NativeLearner:
         if not self.continuous:
             acts = acts.long()
         log_probs, adv, ret = log_probs.reshape(B), adv.reshape(B), ret.reshape(B)
-        mb = B // cfg.num_minibatches
-        perms = np.empty(cfg.num_epochs * B, np.int32)
-        N.numpy_rng_permutations(B, cfg.num_epochs, perms)
-        idx_all = torch.from_numpy(perms.astype(np.int64)).to(self.device).view(
-            cfg.num_epochs, cfg.num_minibatches, mb)
+        E, M = cfg.num_epochs, cfg.num_minibatches
+        Bp = self.perm_n
+        mbp = Bp // M
+        perms = np.empty(E * Bp, np.int32)
+        N.numpy_rng_permutations(Bp, E, perms)
+        perms = perms.reshape(E, M, mbp)
+        if self.global_mb:
+            # this rank's members of each global minibatch (global flat index t * Ng + n)
+            Ng, env0 = Nn * self.world, Nn * self.rank
+            t_, n_ = np.divmod(perms.astype(np.int64), Ng)
+            keep = (n_ >= env0) & (n_ < env0 + Nn)
+            mb_lists = [[torch.from_numpy(t_[e, j][keep[e, j]] * Nn + n_[e, j][keep[e, j]] - env0)
+                         .to(self.device) for j in range(M)] for e in range(E)]
+        else:
+            mb_lists = torch.from_numpy(perms.astype(np.int64)).to(self.device)
         step = step0
-        for b_idx in idx_all:
+        for b_idx in mb_lists:
             for mb_idx in b_idx:
                 self.flat.grad.zero_()
+                # means over this rank's samples, weighted by their share of the global minibatch
+                # (the all-reduce SUM below then yields the reference's global mean)
+                share = (mb_idx.numel() / mbp) if self.global_mb else 1.0 / self.world
+                if mb_idx.numel() == 0:
+                    loss = sum(p.sum() for p in net.parameters()) * 0.0
+                    loss.backward()
+                    if self.world > 1:
+                        torch.distributed.all_reduce(self.flat.grad)
+                    step += 1
+                    N.check(lib.dppo_clip_adam_f32(
+                        self.flat.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
+                        self.v.data_ptr(), self.flat.total, cfg.grad_norm_clip, float(lr), 0.9,
+                        0.999, cfg.adam_eps, step, None, stream), "dppo_clip_adam_f32")
+                    continue
                 if self.continuous:
                     from .continuous_ppo import JointNormal
                     m_, ls_, v_ = net.get_means_log_stds_and_values(obs[mb_idx])
@@ -509,10 +537,11 @@ class NativeLearner:
                 l_v = 0.5 * torch.nn.functional.mse_loss(new_v, ret[mb_idx])
                 ent = dist.entropy().mean()
                 loss = l_pi + cfg.value_loss_weight * l_v + -cfg.entropy_beta * ent
+                if self.world > 1:
+                    loss = loss * share
                 loss.backward()
                 if self.world > 1:
                     torch.distributed.all_reduce(self.flat.grad)
-                    self.flat.grad.div_(self.world)
                 step += 1
                 N.check(lib.dppo_clip_adam_f32(
                     self.flat.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),

@@ -50,6 +50,11 @@ class PPOConfig:
     save_interval: float = 600      # checkpoint interval (seconds)
     verbose: bool = True            # verbose logging
     device_index: int = 0           # GPU ordinal (additive; LOCAL_RANK wins under torchrun)
+    # data parallelism over ranks (additive): False = each rank permutes its own envs' samples and
+    # global minibatch j is the union of the ranks' local minibatches j; True = every rank draws
+    # the reference's permutations of the GLOBAL batch (ppo.py:252-255) and processes its members
+    # of each global minibatch, so N ranks reproduce the single-GPU learn() of the global batch
+    global_minibatches: bool = False
 
 
 class ActorCriticNetwork(nn.Module):
@@ -117,7 +122,10 @@ class _AgentBase:
         self.device = require_gpu(getattr(cfg, "device_index", 0))
         world, rank = dist_world()
         if cfg.seed is not None:                                       # ppo.py:120-122
-            np.random.seed(cfg.seed + rank)  # env-axis shards draw decorrelated minibatch orders
+            # local minibatches: env-axis shards draw decorrelated minibatch orders; global
+            # minibatches: every rank draws the same permutations of the global batch
+            gmb = getattr(cfg, "global_minibatches", False)
+            np.random.seed(cfg.seed + (0 if gmb else rank))
             torch.manual_seed(cfg.seed)
         self.envs = envs if envs is not None else make_vector_env(env_fn, cfg.num_envs)
         obs_space = self.envs.single_observation_space
@@ -264,18 +272,27 @@ class _AgentBase:
 
     def train(self) -> None:
         """Train PPO agent (reference ppo.py:289-312)."""
-        self.current_observations, _ = self.envs.reset(seed=self.cfg.seed)
+        # Under data parallelism each rank's env shard starts from its own seed (the reference's
+        # single process seeds its one vector env with cfg.seed), and only rank 0 writes the
+        # (replicated) checkpoints -- ranks never race on one file.
+        world, rank = dist_world()
+        seed = self.cfg.seed
+        if seed is not None and world > 1:
+            seed = seed + rank * self.cfg.num_envs
+        self.current_observations, _ = self.envs.reset(seed=seed)
+        saves = self.cfg.checkpoint and rank == 0
         last_checkpoint_time = time.time()
         total_rollouts = self.cfg.total_steps // (self.cfg.rollout_steps * self.cfg.num_envs)
+        env_steps = 0
         for rollout_idx in range(total_rollouts):
             experience = self.rollout()
             self.learn(experience)
             env_steps = (rollout_idx + 1) * self.cfg.rollout_steps * self.cfg.num_envs
-            if self.cfg.checkpoint:
+            if saves:
                 if time.time() - last_checkpoint_time >= self.cfg.save_interval:
                     self.checkpointer.save(env_steps, self.network, self.optimizer)
                     last_checkpoint_time = time.time()
-        if self.cfg.checkpoint:
+        if saves:
             self.checkpointer.save(env_steps, self.network, self.optimizer)
         self.envs.close()
 

@@ -239,7 +239,11 @@ class RecurrentPPO:
         self.lr_scheduler.step()
 
     def train(self) -> None:
-        self.current_observations, _ = self.envs.reset(seed=self.cfg.seed)
+        world, rank = dist_world()   # per-rank env seeds, rank-0 checkpoints (as PPO.train)
+        seed = self.cfg.seed
+        if seed is not None and world > 1:
+            seed = seed + rank * self.cfg.num_envs
+        self.current_observations, _ = self.envs.reset(seed=seed)
         self.prev_dones = np.zeros(self.cfg.num_envs, dtype=bool)
         self.current_hx = torch.zeros(1, self.cfg.num_envs, self.cfg.gru_hidden_dim,
                                       device=self.device)
@@ -249,9 +253,9 @@ class RecurrentPPO:
         for i in range(total):
             self.learn(self.rollout())
             env_steps = (i + 1) * self.cfg.rollout_steps * self.cfg.num_envs
-            if self.cfg.checkpoint and time.time() - last >= self.cfg.save_interval:
+            if self.cfg.checkpoint and rank == 0 and time.time() - last >= self.cfg.save_interval:
                 self.checkpointer.save(env_steps, self.network, self.optimizer)
                 last = time.time()
-        if self.cfg.checkpoint:
+        if self.cfg.checkpoint and rank == 0:
             self.checkpointer.save(env_steps, self.network, self.optimizer)
         self.envs.close()

@@ -57,6 +57,15 @@ typedef struct dppo_dims {
   int32_t num_minibatches; /* ppo.py:26 */
   int32_t world_size;      /* ranks sharing the env axis (1 = single GPU) */
   int32_t rank;
+  /* Minibatch semantics across ranks (world_size > 1 only):
+   *  0 = local: each rank permutes its own T*N samples; global minibatch j is the union of the
+   *      ranks' local minibatches j (host_perms: [E][T*N] local indices).
+   *  1 = global: every rank passes the SAME permutations of the global batch (host_perms:
+   *      [E][T*N*world_size], global flat index t*(N*world_size) + n, i.e. what the reference's
+   *      np.random.permutation(B) draws for the whole batch, ppo.py:252-255); each rank processes
+   *      the members of every global minibatch that fall in its env shard [rank*N, (rank+1)*N).
+   *      world_size ranks then reproduce the single-GPU learn of the global batch. */
+  int32_t global_minibatches;
 } dppo_dims;
 
 /* Hyper-parameters of one learn() call (ppo.py:15-37, Adam defaults torch/optim/adam.py:39). */

@@ -116,3 +116,29 @@ def test_learn_trace(name):
         np.testing.assert_allclose(adam["m"][n], z[f"adam/{n}/exp_avg"], rtol=1e-4, atol=1e-8)
         np.testing.assert_allclose(adam["v"][n], z[f"adam/{n}/exp_avg_sq"], rtol=1e-4, atol=1e-10)
     assert adam["step"] == float(z[f"adam/{names[0]}/step"])
+
+
+@pytest.mark.parametrize("name", ["cartpole_small", "lunar_medium", "cheetah_small",
+                                  "pendulum_medium", "lunar_noadvnorm"])
+def test_torch_cpu_restatement_matches_trace(name):
+    """oracle/ppo_torch.py (bench.py's torch-CPU baseline) reproduces the reference's captured
+    learn() traces: same losses, norms and final parameters."""
+    from oracle import ppo_torch as PT
+    z = load_golden(f"learn_{name}.npz")
+    T, N, D, A, cont, n_learn = (int(x) for x in z["dims"])
+    names = list(z["param_names"])
+    params = {n: z["init/" + n].copy() for n in names}
+    hp = _hyper(z)
+    E = hp.num_epochs
+    losses, norms, st = [], [], None
+    for li in range(n_learn):
+        exp = [z[f"exp{li}/" + k] for k in ("obs", "next_obs", "actions", "rewards", "term", "trunc")]
+        tr = PT.learn(params, exp, hp, hp.lr, bool(cont), perms=z["perms"][li * E:(li + 1) * E],
+                      adam_state=st)
+        st = tr["adam_state"]
+        losses += tr["loss"]
+        norms += tr["norm"]
+    np.testing.assert_allclose(losses, z["loss"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(norms, z["norm"], rtol=1e-5, atol=1e-5)
+    for n in names:
+        np.testing.assert_allclose(params[n], z["final/" + n], rtol=0, atol=2e-6, err_msg=n)
