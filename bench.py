@@ -3,27 +3,32 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cartpole4096]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-        --master-port P bench.py --gpus N --steps K --warmup W
+        --master-port P bench.py --gpus N --steps K --warmup W [--config c5]
 
 A "step" is one full PPO.learn() (reference diamond/ppo.py:224-287) over one rollout buffer
 already resident in HBM: old-policy eval, GAE, returns, advantage normalisation, E x M = 32
 minibatch {forward, loss, backward, clip, Adam} steps and the LR-scheduler step.  The minibatch
 permutations are drawn from the global NumPy RNG inside the step, bit-exactly as the reference.
 
-Workload (BASELINE.json configs[1]): CartPole-shaped PPO, T = 128,
-num_envs = 4096 per GPU (weak scaling across GPUs: each rank owns 4096 envs, the gradient is
-all-reduced over RCCL once per minibatch), obs_dim 4, 2 actions, hidden 64, E = 4, M = 8.
-Synthetic data: obs/next_obs ~ N(0,1), rewards ~ N(1,1), term ~ Bern(0.02), trunc ~ Bern(0.005),
-uniform actions, default_rng(rank); random-init weights of the reference architecture.
+Default workload (BASELINE.json configs[1]): CartPole-shaped PPO, T = 128,
+num_envs = 4096 per GPU (weak scaling: each rank owns 4096 envs, the gradient is all-reduced
+over RCCL once per minibatch), obs_dim 4, 2 actions, hidden 64, E = 4, M = 8.  ``--config c5``
+is BASELINE configs[4] as a STRONG-scaling run: 65,536 envs in total split over the ranks
+(8,192 per GPU at 8); its ``update_steps_per_s`` (minibatch optimizer steps per second) is the
+quantity the north star's >= 6x-at-8-GPUs target is stated in.  Synthetic data: obs/next_obs ~
+N(0,1), rewards ~ N(1,1), term ~ Bern(0.02), trunc ~ Bern(0.005), uniform actions,
+default_rng(rank); random-init weights of the reference architecture.
 
 Rank 0 prints ONE JSON line.  ``value`` comes from a timed pass with nothing but the learn()
-work in the stream.  A second timed pass of the same K learns records a HIP event pair on the
-launch stream around every kernel (libdppo timing mode): it yields ``kernels``,
-``device_ms_per_step`` and ``roofline`` -- the dominant kernel (largest share of device time),
-its average launch duration from those events -- and its own ``instrumented_ms_per_step`` (the
-event markers cost stream time, so that pass is never the throughput); ``roofline_gae`` is the GAE kernel at num_envs = 8192
-over 16 rotating buffer sets (368 MB > the 256 MB Infinity Cache).  ``cpu_baseline`` is the
-NumPy oracle (oracle/ppo_np.py) running one full learn() of the same workload on the host.
+work in the stream.  A second timed pass of the same K learns stamps every kernel with its own
+start/end HIP events (libdppo timing mode): ``kernels``, ``device_ms_per_step`` and ``roofline``
+(the dominant kernel by device time, its average launch duration, algorithmic FLOP per launch)
+come from it, never the throughput.  At N = 1 the line also carries ``configs_extra`` (C3
+LunarLander 8192, C4 HalfCheetah 4096 and C5's 65,536 envs on one GPU -- the strong-scaling
+anchor), ``roofline_gae`` (the GAE kernel at num_envs = 8192 over 16 rotating buffer sets, 368 MB
+> the 256 MB Infinity Cache) and ``cpu_baseline``: the PyTorch-CPU restatement of the reference
+path (oracle/ppo_torch.py) timed for one full learn() on the host cores, with the NumPy oracle
+beside it as ``cpu_baseline_numpy``.
 """
 from __future__ import annotations
 
@@ -44,12 +49,16 @@ FP32_PEAK_TFLOPS = 157.3    # MI355X fp32 MFMA (= vector) dense peak
 H = 64
 
 CONFIGS = {
-    # name: (model, T, N per GPU, D, A, continuous, p_term, p_trunc)
-    "cartpole4096": ("CartPole-v1 PPO", 128, 4096, 4, 2, False, 0.02, 0.005),
-    "lunar8192": ("LunarLander-v3 PPO", 128, 8192, 8, 4, False, 0.02, 0.005),
-    "cheetah4096": ("HalfCheetah-v5 ContinuousPPO", 128, 4096, 17, 6, True, 0.0, 0.001),
+    # name: (model, T, N, D, A, continuous, p_term, p_trunc, scaling)
+    #   scaling "weak": N envs per GPU; "strong": N envs in total, split over the ranks
+    "cartpole4096": ("CartPole-v1 PPO", 128, 4096, 4, 2, False, 0.02, 0.005, "weak"),
+    "lunar8192": ("LunarLander-v3 PPO", 128, 8192, 8, 4, False, 0.02, 0.005, "weak"),
+    "cheetah4096": ("HalfCheetah-v5 ContinuousPPO", 128, 4096, 17, 6, True, 0.0, 0.001, "weak"),
     "cartpole8192": ("CartPole-shaped PPO (8,192 envs/GPU: configs[4] shard)", 128, 8192, 4, 2,
-                     False, 0.02, 0.005),
+                     False, 0.02, 0.005, "weak"),
+    # BASELINE configs[4]: 65,536 CartPole-shaped envs in total (8,192 per GPU at 8 GPUs)
+    "c5": ("CartPole-shaped PPO, 65,536 envs in total (configs[4])", 128, 65536, 4, 2, False,
+           0.02, 0.005, "strong"),
 }
 
 
@@ -141,11 +150,10 @@ def gae_roofline(device, T=128, N=8192, sets=16, reps=4):
             "launches": cnt, "rotating_sets": sets}
 
 
-def cpu_baseline(cfg_name, seed=0):
-    """The NumPy oracle's learn() on the same workload, one full step, host cores."""
+def _baseline_inputs(cfg_name, seed=0):
     sys.path.insert(0, ROOT)
     from oracle import ppo_np as P
-    _, T, N, D, A, cont, pt, ptr = CONFIGS[cfg_name]
+    _, T, N, D, A, cont, pt, ptr, _ = CONFIGS[cfg_name]
     rng = np.random.default_rng(seed)
     obs = rng.standard_normal((T, N, D), dtype=np.float32)
     nobs = rng.standard_normal((T, N, D), dtype=np.float32)
@@ -167,57 +175,66 @@ def cpu_baseline(cfg_name, seed=0):
             params[n] = (prng.standard_normal(shapes[n]) / np.sqrt(shapes[n][1])).astype(np.float32)
         else:
             params[n] = np.zeros(shapes[n.replace("bias", "weight")][0], np.float32)
-    adam = P.new_adam_state(params, names)
+    return (obs, nobs, act, rew, te, tr), params, names, cont, T * N
+
+
+def cpu_baselines(cfg_name):
+    """One full learn() of the same workload on the host cores: the PyTorch-CPU restatement
+    (oracle/ppo_torch.py: the reference's own arithmetic -- autograd, torch.distributions,
+    clip_grad_norm_, CPU Adam -- at torch's intra-op thread count) and the NumPy oracle."""
+    from oracle import ppo_np as P
+    from oracle import ppo_torch as PT
+    exp, params, names, cont, B = _baseline_inputs(cfg_name)
+    model = PT.cpu_model()
+    threads = torch.get_num_threads()
+    p1 = {k: v.copy() for k, v in params.items()}
+    torch.optim.Adam([torch.zeros(1, requires_grad=True)])  # first-use imports outside the clock
+    t0 = time.perf_counter()
+    PT.learn(p1, exp, P.Hyper(), 3e-4, cont, rng=np.random.RandomState(42))
+    dt_t = time.perf_counter() - t0
+    torch_b = {"value": round(B / dt_t, 1), "unit": "env-steps/s", "cores": int(threads),
+               "kind": "port", "cpu": model,
+               "sample": f"one full learn() of {cfg_name} (T x N = {B} samples: old-policy eval, "
+                         f"GAE, 4x8 minibatch autograd/clip/Adam steps) by the PyTorch-CPU "
+                         f"restatement of the reference path (oracle/ppo_torch.py), {dt_t:.2f} s "
+                         f"on {threads} torch threads",
+               "seconds": round(dt_t, 3)}
     try:
         from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        np_threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     except Exception:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        np_threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    p2 = {k: v.copy() for k, v in params.items()}
     t0 = time.perf_counter()
-    P.learn(params, adam, (obs, nobs, act, rew, te, tr), P.Hyper(), 3e-4, cont,
+    P.learn(p2, P.new_adam_state(p2, names), exp, P.Hyper(), 3e-4, cont,
             rng=np.random.RandomState(42))
-    dt = time.perf_counter() - t0
-    return {"value": round(T * N / dt, 1), "unit": "env-steps/s", "cores": int(threads),
-            "kind": "port",
-            "sample": f"one full learn() of the same workload (T={T}, N={N}: old-policy eval, "
-                      f"GAE, 4x8 minibatch steps) by the NumPy float32 oracle "
-                      f"(oracle/ppo_np.py), {dt:.2f} s",
-            "seconds": round(dt, 3)}
+    dt_n = time.perf_counter() - t0
+    numpy_b = {"value": round(B / dt_n, 1), "unit": "env-steps/s", "cores": int(np_threads),
+               "kind": "port", "cpu": model,
+               "sample": f"the same learn() by the NumPy float32 oracle (oracle/ppo_np.py), "
+                         f"{dt_n:.2f} s", "seconds": round(dt_n, 3)}
+    return torch_b, numpy_b
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cartpole4096", choices=sorted(CONFIGS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gae-roofline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true",
-                    help="diagnostic: no per-kernel HIP events in the timed region (no roofline)")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
-
+def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=True,
+               global_mb=False):
+    """Time `steps` learn() calls of CONFIGS[name] on this rank; returns the measurement dict
+    (max wall time over ranks)."""
     import diamond
-    model, T, N, D, A, cont, pt, ptr = CONFIGS[args.config]
+    from diamond import _native as NN
+    model, T, Nc, D, A, cont, pt, ptr, scaling = CONFIGS[name]
+    N = Nc // world if scaling == "strong" else Nc
+    if scaling == "strong" and Nc % world:
+        raise SystemExit(f"{name}: {Nc} global envs do not split over {world} ranks")
     Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
     Agent = diamond.ContinuousPPO if cont else diamond.PPO
-    cfg = Cfg(rollout_steps=T, num_envs=N, verbose=False, total_steps=10 ** 12)
+    cfg = Cfg(rollout_steps=T, num_envs=N, verbose=False, total_steps=10 ** 12,
+              global_minibatches=global_mb)
     agent = Agent(None, cfg, envs=SpecEnvs(D, A, cont))
     assert agent._learner.fused, "benchmark must exercise the fused HIP path"
     ro, _ = synth_rollout(T, N, D, A, cont, pt, ptr, seed=rank, device=device)
     torch.cuda.synchronize(device)
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         agent.learn_device(ro)
     torch.cuda.synchronize(device)
     h = agent._learner.handle
@@ -234,7 +251,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             agent.learn_device(ro)
         torch.cuda.synchronize(device)
         if dist is not None:
@@ -251,25 +268,20 @@ def main():
     host = {k: round(hs[k] / max(hs["calls"], 1) * 1e3, 4) for k in ("perms", "enqueue",
                                                                       "draft_start")}
     hits = hs["lookahead_hits"]
-    # Pass B (the per-kernel table and the roofline): the same K learns with a HIP event pair
-    # recorded on the launch stream around every kernel; the markers cost stream time, so this
-    # pass's wall time is reported separately and never as the throughput.
-    from diamond import _native as NN
+    # Pass B (the per-kernel table and the roofline): the same K learns with the kernels' own
+    # start/end HIP events (libdppo timing mode); never the throughput.
     timing = {k: (0.0, 0) for k in NN.TIMING_CLASSES}
     elapsed_instr = None
-    if not args.no_kernel_timing:
+    if kernel_timing:
         elapsed_instr = timed_pass(True)
         timing = h.timing()
     h.set_timing(False)
     loss_trace = agent.learn_trace()
-
+    E, M = cfg.num_epochs, cfg.num_minibatches
     B_global = T * N * world
-    value = B_global * args.steps / elapsed
-    ms_step = elapsed / args.steps * 1e3
-    # dominant kernel by device time in the timed region
     dom = max(timing, key=lambda k: timing[k][0])
     f_eval_full, f_eval_v, f_mb = flops_per_sample(D, A)
-    mb = T * N // cfg.num_minibatches
+    mb = T * N // M
     algo = {  # (bound, algorithmic units per launch, unit)
         "grad": ("mfma", f_mb * mb, "TFLOP/s"),
         "eval": ("mfma", (f_eval_full + f_eval_v) * T * N, "TFLOP/s"),
@@ -290,7 +302,7 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                tr = json.load(open(pmc)).get(args.config, {}).get(dom)
+                tr = json.load(open(pmc)).get(name, {}).get(dom)
                 if tr is not None:
                     roofline["traffic"] = tr
             except Exception:
@@ -299,47 +311,104 @@ def main():
                      "us_avg": round(v[0] / v[1] * 1e3, 2) if v[1] else 0.0}
                  for k, v in timing.items() if v[1]}
     dev_ms = sum(v[0] for v in timing.values())
+    res = {
+        "value": round(B_global * steps / elapsed, 1),
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "update_steps_per_s": round(E * M * steps / elapsed, 1),
+        "scaling": scaling,
+        "config": {"workload": f"{model}: learn() = old-policy eval + GAE + adv-norm + "
+                               f"{E}x{M} minibatch Adam steps", "name": name,
+                   "rollout_steps": T, "num_envs_per_gpu": N, "num_envs_total": N * world,
+                   "obs_dim": D, "act_dim": A, "continuous": cont, "hidden": H,
+                   "batch_per_learn": B_global, "minibatch": B_global // M,
+                   "parallelism": f"env-axis dp{world}",
+                   "minibatches": "global" if (global_mb and world > 1) else
+                                  ("local-union" if world > 1 else "reference")},
+        "roofline": roofline,
+        "kernels": kernel_ms,
+        "device_ms_per_step": round(dev_ms / steps, 4),
+        "instrumented_ms_per_step": (round(elapsed_instr / steps * 1e3, 4)
+                                     if elapsed_instr else None),
+        "host_ms_per_step": host,
+        "perm_lookahead_hits": hits,
+        "final_loss": float(loss_trace[-1, 0]),
+    }
+    del agent, ro
+    torch.cuda.synchronize(device)
+    torch.cuda.empty_cache()
+    return res
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cartpole4096", choices=sorted(CONFIGS))
+    ap.add_argument("--global-minibatches", action="store_true",
+                    help="N > 1: every rank processes its members of the reference's global "
+                         "minibatches (cfg.global_minibatches) instead of local-union minibatches")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gae-roofline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="N = 1: skip the other BASELINE configs (C3, C4, C5 on one GPU)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostic: no per-kernel HIP events in the timed region (no roofline)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    main_res = run_config(args.config, world, rank, dist, device, args.steps, args.warmup,
+                          kernel_timing=not args.no_kernel_timing,
+                          global_mb=args.global_minibatches)
     out = None
     if rank == 0:
         out = {
             "metric": "env-steps/sec (GAE+update) on synthetic [128 x num_envs] buffers",
-            "value": round(value, 1),
+            "value": main_res["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 4),
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": main_res["scaling"],
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"{model}: learn() = old-policy eval + GAE + adv-norm + "
-                                   f"{cfg.num_epochs}x{cfg.num_minibatches} minibatch "
-                                   f"Adam steps", "name": args.config,
-                       "rollout_steps": T, "num_envs_per_gpu": N, "num_envs_total": N * world,
-                       "obs_dim": D, "act_dim": A, "continuous": cont, "hidden": H,
-                       "batch_per_learn": B_global, "minibatch": mb * world,
-                       "parallelism": f"env-axis dp{world}"},
-            "roofline": roofline,
-            "kernels": kernel_ms,
-            "device_ms_per_step": round(dev_ms / args.steps, 4),
-            "instrumented_ms_per_step": (round(elapsed_instr / args.steps * 1e3, 4)
-                                         if elapsed_instr else None),
-            "host_ms_per_step": host,
-            "perm_lookahead_hits": hits,
-            "final_loss": float(loss_trace[-1, 0]),
-            "device": {"name": torch.cuda.get_device_name(device),
-                       "arch": getattr(torch.cuda.get_device_properties(device), "gcnArchName", ""),
-                       "compute_units": torch.cuda.get_device_properties(device).multi_processor_count},
         }
+        out.update({k: v for k, v in main_res.items() if k not in out})
+        out["device"] = {"name": torch.cuda.get_device_name(device),
+                         "arch": getattr(torch.cuda.get_device_properties(device), "gcnArchName", ""),
+                         "compute_units": torch.cuda.get_device_properties(device).multi_processor_count}
+    if world == 1 and not args.no_extra:
+        # the other BASELINE configs on this GPU (C3, C4), and C5's 65,536 global envs on ONE
+        # GPU: the anchor of the configs[4] strong-scaling curve (`--config c5 --gpus N`)
+        extra = {}
+        for name in ("lunar8192", "cheetah4096", "c5"):
+            if name == args.config:
+                continue
+            r = run_config(name, 1, 0, None, device, min(args.steps, 10), 2)
+            extra[name] = {k: r[k] for k in ("value", "ms_per_step", "update_steps_per_s",
+                                             "device_ms_per_step", "host_ms_per_step")}
+            extra[name]["roofline"] = r["roofline"]
+            extra[name]["config"] = r["config"]
+        out["configs_extra"] = extra
     if rank == 0 and world == 1 and not args.no_gae_roofline:
         out["roofline_gae"] = gae_roofline(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(args.config)
-        out["cpu_baseline"] = cb
-        out["speedup_vs_cpu_baseline"] = round(value / cb["value"], 1)
+        tb, nb = cpu_baselines(args.config if args.config != "c5" else "cartpole4096")
+        out["cpu_baseline"] = tb
+        out["cpu_baseline_numpy"] = nb
+        out["speedup_vs_cpu_baseline"] = round(out["value"] / tb["value"], 1)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

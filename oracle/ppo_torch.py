@@ -121,7 +121,7 @@ def learn(params: dict, experience, hp: Hyper = Hyper(), lr: float | None = None
             loss.backward()
             norm = torch.nn.utils.clip_grad_norm_(params_list, hp.grad_norm_clip)   # ppo.py:284
             opt.step()                                                              # ppo.py:285
-            trace["loss"].append(float(loss))
+            trace["loss"].append(float(loss.detach()))
             trace["norm"].append(float(norm))
     with torch.no_grad():
         for n in names:
