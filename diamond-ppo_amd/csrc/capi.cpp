@@ -920,6 +920,17 @@ int dppo_act_f32(dppo_handle* h, const float* params, const float* obs, int64_t 
   return launch_act(h->sh, h->po, params, obs, actions, n, seed, counter, S(stream));
 }
 
+int dppo_actor_forward_f32(dppo_handle* h, const float* params, const float* obs, int64_t n,
+                           float* heads, void* stream) {
+  if (!h || !params || !obs || !heads || n < 0) {
+    set_error("invalid argument to dppo_actor_forward_f32");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(require_mlp(h));
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  return launch_act(h->sh, h->po, params, obs, nullptr, n, 0, 0, S(stream), heads);
+}
+
 int dppo_prepare_f32(dppo_handle* h, const dppo_rollout* rollout, const float* params,
                      const dppo_hparams* hp, const dppo_learn_outputs* outputs, void* stream) {
   if (!h) {

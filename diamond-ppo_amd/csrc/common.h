@@ -192,7 +192,8 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
                 const void* actions, const float* next_obs, float* logp, float* values,
                 float* next_values, int64_t n, hipStream_t s);
 int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
-               void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s);
+               void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s,
+               float* heads = nullptr);
 struct GradArgs {
   const float* params;
   const float* rec;

@@ -371,7 +371,8 @@ struct ActArgs {
   ParamOffsets po;
   const float* params;
   const float* obs;
-  void* actions;
+  void* actions;   // sampled actions, or null (heads only)
+  float* heads;    // optional [n][A]: the logits / Gaussian means the samples are drawn from
   int64_t n;
   uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
   int D, D8, nq1, A;
@@ -424,6 +425,12 @@ __global__ __launch_bounds__(kThreads, 4) void act_kernel(ActArgs a) {
     float out[AMAX];
     heads<AMAX>(out, lds + L.Wo, lds + L.bo, a.A, y, h);
     if (!valid || h != 0) continue;
+    if (a.heads) {
+#pragma unroll
+      for (int k = 0; k < AMAX; ++k)
+        if (k < a.A) a.heads[i * a.A + k] = out[k];
+    }
+    if (!a.actions) continue;
     if (CONT) {
       // Normal(mean, exp(log_std)).sample(): Box-Muller pairs from Philox (4 uniforms per call)
       float* act = (float*)a.actions + i * a.A;
@@ -576,7 +583,8 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
 }
 
 int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
-               void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s) {
+               void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s,
+               float* heads) {
   if (n <= 0) return DPPO_OK;
   ActArgs k{};
   k.L = make_layout(sh);
@@ -584,6 +592,7 @@ int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, 
   k.params = params;
   k.obs = obs;
   k.actions = actions;
+  k.heads = heads;
   k.n = n;
   k.seed_lo = (uint32_t)seed;
   k.seed_hi = (uint32_t)(seed >> 32);

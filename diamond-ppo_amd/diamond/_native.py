@@ -29,7 +29,7 @@ EXPORTED = [
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
     "dppo_perm_targets_numpy", "dppo_perm_resolve", "dppo_act_f32", "dppo_loopback_group",
-    "dppo_status", "dppo_fanin_selftest",
+    "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
                   "allreduce", "perm", "reduce_adam"]
@@ -114,6 +114,7 @@ def load():
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
         "dppo_loopback_group": (ctypes.c_int, [P(vp), i32]),
         "dppo_status": (ctypes.c_int, [vp]),
+        "dppo_actor_forward_f32": (ctypes.c_int, [vp, vp, vp, i64, vp, vp]),
         "dppo_fanin_selftest": (ctypes.c_int, [vp, i32, i32, i64, vp]),
         "dppo_set_timing": (ctypes.c_int, [vp, i32]),
         "dppo_get_timing": (ctypes.c_int, [vp, vp, vp]),

@@ -11,9 +11,9 @@ are drawn on a host thread while learn k is enqueued and runs, from the RNG stat
 behind (``dppo_perm_numpy``: one sequential MT19937 stream, each epoch's Fisher-Yates swaps on a
 worker thread of their own).  Learn k+1 uses them only if the global NumPy RNG still holds
 exactly that state (otherwise it draws afresh), so results and the RNG stream stay bit-identical
-to the reference's.  With ``DPPO_PERM_DEVICE=1`` the host only draws the swap targets and the GPU
-resolves the swaps (``shuffle.hip``, ``dppo_learn_targets_f32``) -- for hosts too slow to hide
-the swaps.
+to the reference's.  For large batches (E*B >= 2^23 entries, or ``DPPO_PERM_DEVICE=1``) the host
+only draws the swap targets and the GPU resolves the swaps (``shuffle.hip``,
+``dppo_learn_targets_f32``): the host swap chain is cache-miss bound at those sizes.
 
 Two paths, chosen once per agent:
 
@@ -280,8 +280,38 @@ def hparams(cfg, lr: float, adam_step: int, betas=(0.9, 0.999)) -> N.HParams:
 
 
 # ---------------------------------------------------------------------------------------------
+class _DraftWorker:
+    """One long-lived host thread that draws the next learn's permutations (a thread per learn
+    cost ~0.7 ms of start-up on the launching thread).  ctypes releases the GIL during the draw."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._job = None
+        self._thread = threading.Thread(target=self._run, name="dppo-perm-draft", daemon=True)
+        self._thread.start()
+
+    def submit(self, fn, done: threading.Event):
+        with self._cv:
+            self._job = (fn, done)
+            self._cv.notify()
+
+    def _run(self):
+        while True:
+            with self._cv:
+                while self._job is None:
+                    self._cv.wait()
+                fn, done = self._job
+                self._job = None
+            try:
+                fn()
+            finally:
+                done.set()
+
+
 class NativeLearner:
     """Binds one agent (network + Adam) to a libdppo handle for its rollout shape."""
+
+    PERM_DEVICE_MIN = 1 << 23  # E*B permutation entries above which the GPU resolves the swaps
 
     def __init__(self, network, optimizer, cfg, obs_dim, act_dim, continuous, device,
                  network_is_default: bool):
@@ -324,9 +354,17 @@ class NativeLearner:
         self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "calls": 0,
                              "lookahead_hits": 0}
         self.lookahead = os.environ.get("DPPO_PERM_LOOKAHEAD", "1") != "0"
-        self.device_shuffle = os.environ.get("DPPO_PERM_DEVICE", "0") == "1"
+        # Where the Fisher-Yates swaps run.  The host's swap chain is cache-miss bound once the
+        # [E][B] permutations outgrow the caches (C5 on one GPU, E*B = 33.5 M: ~46 ms of host
+        # time per learn against ~32 ms of device time), so above PERM_DEVICE_MIN entries the
+        # host only draws the MT19937 swap targets and the GPU resolves the swaps (shuffle.hip,
+        # bit-identical).  DPPO_PERM_DEVICE=0/1 forces either side.
+        env = os.environ.get("DPPO_PERM_DEVICE")
+        self.device_shuffle = (env == "1") if env in ("0", "1") else (
+            cfg.num_epochs * self.perm_n >= self.PERM_DEVICE_MIN)
         self._draft = None
         self._slot = 0
+        self._worker = None
 
     def _init_comm(self):
         d = torch.distributed
@@ -374,11 +412,11 @@ class NativeLearner:
         return out.copy() if self.continuous else out.astype(np.int64)
 
     def _start_draft(self, key: np.ndarray, pos: int):
-        """Draw the next learn's swap targets on a host thread (ctypes releases the GIL)."""
+        """Draw the next learn's permutations (or swap targets) on the draft worker thread."""
         slot = 1 - self._slot
         buf = self.handle.perm_buffer(slot)
         d = {"slot": slot, "buf": buf, "key_in": key.copy(), "pos_in": pos, "ok": False,
-             "device": self.device_shuffle}
+             "device": self.device_shuffle, "done": threading.Event()}
 
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
 
@@ -388,8 +426,9 @@ class NativeLearner:
             d["key_out"] = k
             d["ok"] = True
 
-        d["thread"] = threading.Thread(target=work, name="dppo-perm-draft", daemon=True)
-        d["thread"].start()
+        if self._worker is None:
+            self._worker = _DraftWorker()
+        self._worker.submit(work, d["done"])
         self._draft = d
 
     def _targets(self):
@@ -399,7 +438,7 @@ class NativeLearner:
         key, pos, st = N.mt_state()
         d, self._draft = self._draft, None
         if d is not None:
-            d["thread"].join()
+            d["done"].wait()
             if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos
                     and np.array_equal(d["key_in"], key)):
                 self._slot = d["slot"]

@@ -151,6 +151,12 @@ int dppo_old_policy_f32(dppo_handle* h, const float* params, const float* obs, c
 int dppo_act_f32(dppo_handle* h, const float* params, const float* obs, int64_t n, uint64_t seed,
                  uint64_t counter, void* actions, void* stream);
 
+/* The actor half of dppo_act_f32 without the draw: the logits (discrete, ppo.py:79) or Gaussian
+ * means (continuous, continuous_ppo.py:88-90) of the default actor for obs [n][D], written to
+ * heads [n][A] -- exactly the values dppo_act_f32 samples from. */
+int dppo_actor_forward_f32(dppo_handle* h, const float* params, const float* obs, int64_t n,
+                           float* heads, void* stream);
+
 /* One full PPO.learn (ppo.py:224-287 / continuous_ppo.py:236-299) with the default network:
  * old-policy eval, GAE, returns, advantage normalisation, then num_epochs x num_minibatches
  * {gather, forward, clipped-surrogate + value + entropy loss, analytic backward, [RCCL

@@ -336,3 +336,26 @@ def learn(params, adam, experience, hp: Hyper, lr, continuous=False, perms=None,
                 trace["params"].append(np.concatenate([params[n].ravel() for n in names]))
     trace.update(old_logp=logp, values=values, next_values=nvals, adv_raw=None)
     return trace
+
+
+# ---------------------------------------------------------------------------------------------
+# tanh-squashed Gaussian.  The reference has NO squash (continuous_ppo.py:83-111
+# sample and score the raw Gaussian); BASELINE names a "tanh-squash kernel path" for HalfCheetah,
+# which this build offers as an opt-in extension (ContinuousPPOConfig.tanh_squash).  Restated here
+# so the extension has a CPU yardstick: env action and log-density of a = tanh(u).
+# ---------------------------------------------------------------------------------------------
+def squash_action(u, low, high):
+    """Env action for the Gaussian sample u: tanh(u) rescaled from [-1, 1] to [low, high]."""
+    u = np.asarray(u, np.float64)
+    return low + (np.tanh(u) + 1.0) * 0.5 * (high - low)
+
+
+def squashed_normal_logp(mean, log_std, u):
+    """log-density of a = tanh(u), u ~ N(mean, exp(log_std)), summed over action dims, in float64:
+    log N(u; mean, sigma) - sum_a log(1 - tanh(u_a)^2) (change of variables)."""
+    mean = np.asarray(mean, np.float64)
+    log_std = np.asarray(log_std, np.float64)
+    u = np.asarray(u, np.float64)
+    sigma = np.exp(log_std)
+    base = (-((u - mean) ** 2) / (2 * sigma * sigma) - log_std - LOG_SQRT_2PI).sum(-1)
+    return base - np.log1p(-np.tanh(u) ** 2).sum(-1)

@@ -18,6 +18,9 @@ What is captured (SURVEY.md §8(c) "Golden vectors to generate & commit"):
                         Adam state.  Some traces call learn() twice (Adam step / RNG continuation,
                         decay_lr).
 * perm_seed42.npz    -- numpy legacy RandomState permutations (ppo.py:120-122,254).
+* ckpt_cartpole-step000128.pt + ckpt_cartpole_resume.npz -- a checkpoint written by the
+                        reference's Checkpointer.save after one learn(), and the learn() of a fresh
+                        reference agent resumed from it (utils.py:584-612).
 
 Capture is done by wrapping bound methods / module attributes at call time; no reference
 file is modified.
@@ -294,11 +297,68 @@ def make_perm_golden():
     print("perm_seed42.npz; first 8 of permutation(1024):", p1024[:8])
 
 
+def make_checkpoint_fixture(diamond, gym_stub):
+    """A checkpoint written by the reference's own Checkpointer.save (utils.py:584-600) after one
+    learn(), and the trace of a FRESH reference agent that Checkpointer.load-s it (utils.py:602-612)
+    and learns on a second rollout: the oracle for resuming from a reference checkpoint.  The .pt
+    holds only tensors, numbers and dicts/lists (loadable with torch.load(weights_only=True))."""
+    import shutil
+    import tempfile
+    from diamond.utils import Checkpointer
+    T, N, D, A = 8, 16, 4, 2
+    cfg = diamond.PPOConfig(rollout_steps=T, num_envs=N, verbose=False)
+    env_fn = lambda: gym_stub.SyntheticEnv(D, A)
+    rng = np.random.default_rng(2024)
+    a1 = diamond.PPO(env_fn, cfg=cfg)
+    a1.learn(synth_experience(rng, T, N, D, A, False, 0.1, 0.05))
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        ck = Checkpointer(folder=d, run_name="golden")
+        ck.save(T * N, a1.network, a1.optimizer)
+        src = os.path.join(d, f"golden-step{T * N:06d}.pt")
+        dst = os.path.join(HERE, "ckpt_cartpole-step000128.pt")
+        shutil.copyfile(src, dst)
+    a2 = diamond.PPO(env_fn, cfg=cfg)          # fresh agent: its own init, then the checkpoint
+    Checkpointer().load(dst, a2.network, a2.optimizer)
+    exp = synth_experience(rng, T, N, D, A, False, 0.1, 0.05)
+    for i, k in enumerate(("obs", "next_obs", "actions", "rewards", "term", "trunc")):
+        out[f"exp/{k}"] = np.asarray([row[i] for row in exp])
+    st = np.random.get_state()
+    out["rng_state"] = np.array(st[1])
+    out["rng_pos"] = np.array(st[2])
+    losses = []
+    real_backward = torch.Tensor.backward
+
+    def backward_wrap(self, *a, **k):
+        losses.append(float(self.detach()))
+        return real_backward(self, *a, **k)
+
+    torch.Tensor.backward = backward_wrap
+    try:
+        a2.learn(exp)
+    finally:
+        torch.Tensor.backward = real_backward
+    out["loss"] = np.array(losses)
+    out["param_names"] = np.array([n for n, _ in a2.network.named_parameters()])
+    for n, p in a2.network.named_parameters():
+        out[f"final/{n}"] = p.detach().numpy().copy()
+    for n, p in a2.network.named_parameters():
+        stt = a2.optimizer.state[p]
+        out[f"adam/{n}/exp_avg"] = stt["exp_avg"].numpy().copy()
+        out[f"adam/{n}/step"] = np.array(float(stt["step"]))
+    np.savez_compressed(os.path.join(HERE, "ckpt_cartpole_resume.npz"), **out)
+    print("ckpt_cartpole-step000128.pt + ckpt_cartpole_resume.npz:", len(losses), "steps after load")
+
+
 def main():
     if not os.path.isdir(REF):
         raise SystemExit("reference not present; fixtures are generated only in the survey container")
     torch.set_num_threads(8)
     gym_stub, diamond, ref_ppo, ref_cppo = _import_reference()
+    if sys.argv[1:] == ["checkpoint"]:
+        make_checkpoint_fixture(diamond, gym_stub)
+        return
+    make_checkpoint_fixture(diamond, gym_stub)
     make_perm_golden()
     make_gae_cases(diamond, gym_stub)
     make_learn_trace(diamond, gym_stub, "cartpole_small", continuous=False, T=8, N=16, D=4, A=2,

@@ -31,7 +31,7 @@ NI = len(NAMES0)  # barriers per interval set
 
 def main():
     # PHASE_CONFIG: a bench.py config name (default cartpole4096)
-    _, T, Nn, D, A, cont, pt, ptr = bench.CONFIGS[os.environ.get("PHASE_CONFIG", "cartpole4096")]
+    _, T, Nn, D, A, cont, pt, ptr, _ = bench.CONFIGS[os.environ.get("PHASE_CONFIG", "cartpole4096")]
     Nn = int(os.environ.get("ABL_N", Nn))
     Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
     Agent = diamond.ContinuousPPO if cont else diamond.PPO
