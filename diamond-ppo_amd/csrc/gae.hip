@@ -154,8 +154,10 @@ __global__ __launch_bounds__(kThreads) void gae_kernel(
 //    (16-B stores) and accumulates the normalisation statistics;
 //  * wave 8 is the scan (lane = env): per chunk 8 ds_read_b128, then 16 dependent steps of
 //    a = delta + coef * a (two VALU ops each), 4 ds_write_b128; fully unrolled over the 8 chunks
-//    so the chain waits only for its own chunk's reads (1.2 us faster than the rolled loop, whose
-//    loop-carried register copies made every chunk wait for the next chunk's prefetch).
+//    with the operands of the next two chunks already requested, so the chain waits only for
+//    reads issued two chunks earlier (the rolled loop's loop-carried register copies made every
+//    chunk wait for the next chunk's prefetch: 1.2 us; one chunk of look-ahead still exposed the
+//    LDS latency under the owners' traffic: ~650 cycles per chunk).
 // Timing-only builds: DPPO_GAE_TRACE (hand-off timeline, tools/gae_trace.py), DPPO_GAE_NOSCAN
 // (no recurrence: the movement-only time of this structure, wrong results).
 // An owner that has stored its chunk of tile i goes straight on to its chunk of tile i + 1, so
@@ -204,6 +206,13 @@ __device__ __forceinline__ void gae_terms(float r, float v, float nv, float te, 
   coef = (c * nt) * ntr;                      // ppo.py:214-218
 }
 
+// 16-B store written through to memory (sc1): the line leaves the XCD's L2 while the kernel runs
+// instead of as a dirty line written back at the kernel boundary (MI355X_MICROARCH.md
+// publish-large / boundary: a predecessor leaving B dirty bytes costs ~B / 6 TB/s)
+__device__ __forceinline__ void store_wt(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 __device__ __forceinline__ float gae_carry(float delta, float coef, float a) {
 #pragma clang fp contract(off)
   return delta + coef * a;                    // ppo.py:213-219
@@ -245,7 +254,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ val,
     const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
-    double* __restrict__ partials, int T, int N, float g, float c) {
+    double* __restrict__ partials, int T, int N, float g, float c, int wt) {
   __shared__ __attribute__((aligned(16))) PipeLds<E> L;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ntiles = N / E;
@@ -325,8 +334,13 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
             f32x4 av;
 #pragma unroll
             for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
-            *(f32x4*)(adv + go) = av;
-            *(f32x4*)(ret + go) = xv[p] + av;  // returns = values + advantages (ppo.py:241)
+            if (wt) {
+              store_wt(adv + go, av);
+              store_wt(ret + go, xv[p] + av);  // returns = values + advantages (ppo.py:241)
+            } else {
+              *(f32x4*)(adv + go) = av;
+              *(f32x4*)(ret + go) = xv[p] + av;
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               lsum += (double)av[j];
@@ -349,37 +363,52 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     }
   } else if (lane < E) {
     // ---------------- the scan, one lane per env, all kPChunks chunks of every super-chunk
-    // (missing ones are identity rows), fully unrolled: the operands of chunk k sit in one of two
-    // static register sets while chunk k-1's are read into the other, so the chain waits only
-    // for its own chunk's LDS reads.
+    // (missing ones are identity rows), fully unrolled over three static operand register sets:
+    // while chunk k's 16 dependent steps run, chunk k-1's operands are already in registers and
+    // chunk k-2's LDS reads are in flight -- the chain never waits for reads issued during the
+    // previous chunk (with one chunk of look-ahead it did: ~650 cycles per 16-step chunk under
+    // the owners' LDS traffic, against ~250 now).
     const int e = lane;
     int gen = 0;
+    // The scan is the youngest wave of the workgroup and shares its SIMD with two owners: at the
+    // default priority every owner VALU instruction issues first (age order) and the dependent
+    // chain crawls at ~30 cycles per step.  It is the critical path: give it the SIMD.
+    __builtin_amdgcn_s_setprio(3);
     for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
       float a = 0.0f;  // advantage carried backwards, 0 after the last step (ppo.py:198)
       for (int s = 0; s < nsup; ++s) {
         ++gen;
-        f32x4 d[2][4], cf[2][4];
-        wait_flag(&L.loaded[kPChunks - 1], gen);
+        f32x4 d[3][4], cf[3][4];
+        int pf[kPChunks];  // the chunk flag seen just before its speculative prefetch
+        auto fetch = [&](int k, int set) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          d[(kPChunks - 1) & 1][q] = *(const f32x4*)&L.delta[e][(kPChunks - 1) * kPChunk + 4 * q];
-          cf[(kPChunks - 1) & 1][q] = *(const f32x4*)&L.coef[e][(kPChunks - 1) * kPChunk + 4 * q];
-        }
+          for (int q = 0; q < 4; ++q) {
+            d[set][q] = *(const f32x4*)&L.delta[e][k * kPChunk + 4 * q];
+            cf[set][q] = *(const f32x4*)&L.coef[e][k * kPChunk + 4 * q];
+          }
+        };
+        wait_flag(&L.loaded[kPChunks - 1], gen);
+        pf[kPChunks - 1] = gen;
+        fetch(kPChunks - 1, (kPChunks - 1) % 3);
+        // speculative prefetch of chunk k-1 / k-2: its flag is read before its data (LDS
+        // operations of one wave complete in order), so a set flag proves the data current
+        pf[kPChunks - 2] =
+            __hip_atomic_load(&L.loaded[kPChunks - 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_sched_barrier(0);
+        fetch(kPChunks - 2, (kPChunks - 2) % 3);
 #pragma unroll
         for (int k = kPChunks - 1; k >= 0; --k) {
-          const int b = k & 1;
+          const int b = k % 3;
           GAE_STAMP(25 + k);
-          // speculative prefetch of chunk k-1: its flag is read before its data (LDS operations of
-          // one wave complete in order), so a set flag proves the prefetched data is current
-          int pf = gen;
-          if (k > 0) {
-            pf = __hip_atomic_load(&L.loaded[k - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (k >= 2) {
+            pf[k - 2] = __hip_atomic_load(&L.loaded[k - 2], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              d[b ^ 1][q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
-              cf[b ^ 1][q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
-            }
+            fetch(k - 2, (k - 2) % 3);
+          }
+          if (pf[k] < gen) {  // prefetched before its owner published it: wait and re-read
+            wait_flag(&L.loaded[k], gen);
+            fetch(k, b);
           }
 #ifndef DPPO_GAE_NOSCAN
           f32x4 av[4];
@@ -393,14 +422,6 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
 #endif
           if (lane == 0) set_flag(&L.scanned[k], gen);
           GAE_STAMP(33 + k);
-          if (k > 0 && pf < gen) {
-            wait_flag(&L.loaded[k - 1], gen);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              d[b ^ 1][q] = *(const f32x4*)&L.delta[e][(k - 1) * kPChunk + 4 * q];
-              cf[b ^ 1][q] = *(const f32x4*)&L.coef[e][(k - 1) * kPChunk + 4 * q];
-            }
-          }
         }
       }
     }
@@ -566,16 +587,18 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     static const int per_cu =
         std::getenv("DPPO_GAE_WGS_PER_CU") ? std::atoi(std::getenv("DPPO_GAE_WGS_PER_CU")) : 1;
     const bool e32 = env_e == 32 ? N % 32 == 0 : (env_e == 16 ? false : (N % 32 == 0 && N / 32 >= cus));
+    // DPPO_GAE_WT=0/1: plain or write-through (sc1) advantage / return stores (A/B timing)
+    static const int wt = std::getenv("DPPO_GAE_WT") ? std::atoi(std::getenv("DPPO_GAE_WT")) : 0;
     const int tiles = e32 ? N / 32 : G;
     int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
     if (!e32 && grid >= 16) grid -= grid % 16;
     *n_partials = grid;
     if (e32)
       DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c);
+                  adv, ret, partials, T, N, gamma, c, wt);
     else
       DPPO_LAUNCH(gae_pipe_kernel<16>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c);
+                  adv, ret, partials, T, N, gamma, c, wt);
   } else if (vec)
     DPPO_LAUNCH(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
                        partials, T, N, gamma, c);

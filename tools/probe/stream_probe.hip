@@ -5,6 +5,13 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// 16-B store written through to memory (sc1: the line leaves the XCD's L2 while the kernel runs
+// instead of as a dirty line at the kernel boundary; MI355X_MICROARCH.md publish-large)
+__device__ __forceinline__ void store_wt(f32x4* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <bool WT>
 __global__ __launch_bounds__(256) void stream_kernel(const float* __restrict__ r,
                                                      const uint8_t* __restrict__ te,
                                                      const uint8_t* __restrict__ tr,
@@ -18,17 +25,26 @@ __global__ __launch_bounds__(256) void stream_kernel(const float* __restrict__ r
     const f32x4 c = ((const f32x4*)nv)[i];
     const uint32_t t = ((const uint32_t*)te)[i];
     const uint32_t u = ((const uint32_t*)tr)[i];
-    ((f32x4*)adv)[i] = a + b;
     f32x4 o = c;
     o[0] += (float)((t ^ u) & 0xff);
-    ((f32x4*)ret)[i] = o;
+    if (WT) {
+      store_wt((f32x4*)adv + i, a + b);
+      store_wt((f32x4*)ret + i, o);
+    } else {
+      ((f32x4*)adv)[i] = a + b;
+      ((f32x4*)ret)[i] = o;
+    }
   }
 }
 
 extern "C" int probe_stream(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
                             const float* nv, float* adv, float* ret, int64_t n, int grid,
-                            void* stream) {
-  hipLaunchKernelGGL(stream_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, r, te, tr, v,
-                     nv, adv, ret, n / 4);
+                            void* stream, int write_through) {
+  if (write_through)
+    hipLaunchKernelGGL(stream_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, r, te,
+                       tr, v, nv, adv, ret, n / 4);
+  else
+    hipLaunchKernelGGL(stream_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, r, te,
+                       tr, v, nv, adv, ret, n / 4);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
