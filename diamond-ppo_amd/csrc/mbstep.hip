@@ -55,11 +55,27 @@ constexpr float kHalfLog2PiPlusHalf = 1.41893853320467274178f;
 // Timing-only ablation switches (tools/ablate.py); a shipped build defines none of them.
 #ifdef DPPO_ABL_NOBARRIER
 #define STEP_BARRIER() __builtin_amdgcn_wave_barrier()
+#define HEAD_STAMP(k) \
+  do {                \
+  } while (0)
 #elif defined(DPPO_PHASE_TRACE)
 // Timing-only build: workgroup 0 records, per wave and per barrier, the cycle counter when the
 // wave arrives (its phase work issued and drained) and when the barrier releases it.
 constexpr int kTraceBars = 128;
 __device__ long long g_phase_trace[kTraceBars][kThreads / 64][2];
+// per workgroup: s_memtime at entry, loop entry, loop exit, epilogue drained; s_memrealtime at
+// entry and at the end (cross-CU skew)
+__device__ long long g_phase_edges[256][6];
+#define EDGE_STAMP(i)                                                                 \
+  do {                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 256)                                         \
+      g_phase_edges[blockIdx.x][i] = __builtin_amdgcn_s_memtime();                    \
+  } while (0)
+#define EDGE_REAL(i)                                                                  \
+  do {                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 256)                                         \
+      g_phase_edges[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();                \
+  } while (0)
 __device__ long long g_heads_trace[kTraceBars][4];
 #define HEAD_STAMP(k)                                                                   \
   do {                                                                                  \
@@ -82,6 +98,14 @@ __device__ long long g_heads_trace[kTraceBars][4];
 #define STEP_BARRIER() __syncthreads()
 #define HEAD_STAMP(k) \
   do {                \
+  } while (0)
+#endif
+#ifndef EDGE_STAMP
+#define EDGE_STAMP(i) \
+  do {                \
+  } while (0)
+#define EDGE_REAL(i) \
+  do {               \
   } while (0)
 #endif
 
@@ -212,6 +236,10 @@ __device__ void fused_reduce_adam(const MArgs& a, float* lds) {
 
 inline int a4(int x) { return (x + 3) & ~3; }
 
+__device__ __forceinline__ void zero_image(float* img, int n4, int tid) {
+  for (int c = tid; c < n4; c += kThreads) ((f32x4*)img)[c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+}
+
 Lds2 make_lds2(int D16) {
   Lds2 L{};
   int o = 0;
@@ -259,13 +287,25 @@ __device__ __forceinline__ float* opaque_base(float* p) {
 // XCD L2s while the kernel runs instead of as dirty lines at the kernel boundary, and the reduce
 // kernel (other XCDs) reads them from memory either way (MI355X_MICROARCH.md: boundary,
 // publish-large).
-__device__ __forceinline__ void slab_put(float* p, float v) {
+__device__ __forceinline__ void slab_put4(float* p, f32x4 v) {
 #ifdef DPPO_ABL_PLAINSLAB
-  *p = v;
+  *(f32x4*)p = v;
 #else
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 #endif
 }
+
+// Register-slice staging of the hidden weights (prologue): W2, Wa, Wc land in LDS through
+// coalesced 16-B loads (every workgroup reads the same 48 KB: one request per 1 KB wave-load
+// instead of sixteen 16-B pieces per 4-B lane load), rows padded to kStageRow floats so that both
+// the row slices of the forward team (lane (l15, h4) reads row 16q + l15, columns 4t + h4) and the
+// column slices of the backward team (row 4t + h4, column 16q + l15) are near conflict-free b32
+// reads (kStageRow = 18 mod 32).
+constexpr int kStageRow = 82;
+constexpr int kStageFloats = 3 * H * kStageRow;
+// The epilogue assembles the workgroup's gradient slab in LDS (after the head-partial scratch of
+// the forward team) and writes it out as 16-B write-through stores.
+constexpr int kEpiHead = kTeamWaves * (16 + 3) * 64;
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -456,6 +496,13 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
   const int nsteps = (mm + S - 1) / S;
   const int nit = (nsteps + (int)gridDim.x - 1) / (int)gridDim.x;  // steps per workgroup
   float* slab = a.slabs + (int64_t)blockIdx.x * a.slab_stride;
+  EDGE_STAMP(0);
+  EDGE_REAL(4);
+  // forward team: the first step's sample index before anything else (its record gather waits on
+  // it); lane group (lane >> 3) of wave q takes sample 8 q + (lane >> 3) of a step
+  const int hs = SPW * q + (lane >> 3);
+  int nidx0 = 0;
+  if (team == 0 && nit > 0 && (int)blockIdx.x * S + hs < mm) nidx0 = idxp[(int)blockIdx.x * S + hs];
 
   // ---------------- prologue: LDS head weights / biases
   for (int k = tid; k < 16 * H; k += kThreads) {
@@ -497,6 +544,23 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     }
   }
 
+  {
+    // W2 | Wa | Wc -> padded LDS image (the step-image area, unused until the main loop)
+    float* stg = lds_ + L.H1[0];
+    for (int k = tid; k < 3 * H * H / 4; k += kThreads) {
+      const int m = k >> 10, e = k & 1023, row = e >> 4, c4 = e & 15;
+      const int off = m == 0 ? po.W2 : (m == 1 ? po.Wa : po.Wc);
+      const f32x4 v = *(const f32x4*)(P + off + row * H + 4 * c4);
+      float* d = stg + m * H * kStageRow + row * kStageRow + 4 * c4;
+      *(f32x2*)d = (f32x2){v[0], v[1]};
+      *(f32x2*)(d + 2) = (f32x2){v[2], v[3]};
+    }
+  }
+  __syncthreads();
+  const float* stg = lds_ + L.H1[0];
+  float* img = lds_ + kEpiHead;                       // epilogue: this workgroup's slab image
+  const int nimg4 = (int)((a.p_total + 8 + 3) / 4);   // parameters + loss slots, in f32x4
+
   if (team == 0) {
     // =========================== forward team ===========================
     float w1f[8], w2f[16], waf[16], wcf[16];
@@ -508,9 +572,10 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const int k = 4 * t + h4;
-      w2f[t] = P[po.W2 + (row0 + l15) * H + k];
-      waf[t] = P[po.Wa + (row0 + l15) * H + k];
-      wcf[t] = P[po.Wc + (row0 + l15) * H + k];
+      const int o = (row0 + l15) * kStageRow + k;
+      w2f[t] = stg[o];
+      waf[t] = stg[H * kStageRow + o];
+      wcf[t] = stg[2 * H * kStageRow + o];
     }
     f32x4 gba = (f32x4){0.f, 0.f, 0.f, 0.f}, gbc = gba;  // hidden-bias partials (ba, bc rows)
     float gWo[AMAX];
@@ -518,7 +583,6 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     for (int k = 0; k < AMAX; ++k) gWo[k] = 0.f;
     float gWv = 0.f, gbh = 0.f, s_pi = 0.f, s_v = 0.f, s_ent = 0.f;
     const int hj = lane & 7;             // 8 lanes per sample
-    const int hs = SPW * q + (lane >> 3);  // this lane group's sample within the step
 
     // Sample-record prefetch: after the heads of step it the records of step it+1 (observation
     // chunk, {action, old log-prob, advantage, return}, continuous actions) and the indices of step
@@ -554,7 +618,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         for (int j = 0; j < 4; ++j) X0[hs * SX0 + perm(kb + j)] = pobs[j];
       }
     };
-    load_idx(0);
+    nidx = nidx0;  // load_idx(0), issued at kernel entry
     load_rec(0);
     csc = psc;
 #pragma unroll
@@ -562,6 +626,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     gather(0);
     load_idx(1);
     __syncthreads();  // LDS head weights / biases and X0 of step 0 visible
+    EDGE_STAMP(1);
     // Up to 4 actions the head weights this lane touches are loop-invariant registers: in the
     // head phase lane hj covers permuted columns [4hj, 4hj+4) and [32+4hj, 32+4hj+4) of a
     // sample; in the head back-propagation it covers the permuted columns of its own rows.
@@ -869,8 +934,11 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       STEP_BARRIER();
     }
 
-    // ---- epilogue (forward team): actor/critic hidden-bias rows straight to the slab; head
+    EDGE_STAMP(2);
+    // ---- epilogue (forward team): actor/critic hidden-bias rows into the slab image; head
     // partials and loss sums combined over the 4 waves through LDS in a fixed order
+    zero_image(img, nimg4, tid);
+    __syncthreads();  // (Z) the image is zero: padding floats stay zero in the slab
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float va = gba[r], vc = gbc[r];
@@ -880,8 +948,8 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         vc += __shfl_xor(vc, off);
       }
       if (l15 == 0) {
-        slab_put(slab + (po.ba + row0 + 4 * h4 + r), va);
-        slab_put(slab + (po.bc + row0 + 4 * h4 + r), vc);
+        img[po.ba + row0 + 4 * h4 + r] = va;
+        img[po.bc + row0 + 4 * h4 + r] = vc;
       }
     }
     for (int off = 32; off >= 1; off >>= 1) {
@@ -896,7 +964,7 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     hp[AMAX * 64 + lane] = gWv;
     hp[(AMAX + 1) * 64 + lane] = gbh;
     hp[(AMAX + 2) * 64 + lane] = lane == 0 ? s_pi : (lane == 1 ? s_v : (lane == 2 ? s_ent : 0.f));
-    // rendezvous: team 1 joins this barrier after its own (LDS-free) epilogue
+    // (R) rendezvous: team 1 joins this barrier after writing its accumulators into the image
     __syncthreads();
     const int c15 = lane & 15;
     const int ftrue = (lane & ~15) + 4 * (c15 & 3) + (c15 >> 2);  // true feature of column lane
@@ -904,15 +972,15 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
       const float v = ((lds_[(0 * NH + e) * 64 + lane] + lds_[(1 * NH + e) * 64 + lane]) +
                        lds_[(2 * NH + e) * 64 + lane]) + lds_[(3 * NH + e) * 64 + lane];
       if (e < AMAX) {
-        if (e < a.A) slab_put(slab + (po.Wo + e * H + ftrue), v);
+        if (e < a.A) img[po.Wo + e * H + ftrue] = v;
       } else if (e == AMAX) {
-        slab_put(slab + (po.Wv + ftrue), v);
+        img[po.Wv + ftrue] = v;
       } else if (e == AMAX + 1) {
-        if (lane < a.A) slab_put(slab + (po.bo + lane), v);
-        if (lane == 32) slab_put(slab + (po.bv), v);
-        if (CONT && lane >= 33 && lane < 33 + a.A) slab_put(slab + (po.ls + (lane - 33)), v);
+        if (lane < a.A) img[po.bo + lane] = v;
+        if (lane == 32) img[po.bv] = v;
+        if (CONT && lane >= 33 && lane < 33 + a.A) img[po.ls + (lane - 33)] = v;
       } else {
-        if (lane < 3) slab_put(slab + (a.p_total + lane), v);
+        if (lane < 3) img[a.p_total + lane] = v;
       }
     }
   } else {
@@ -921,9 +989,10 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const int k = 4 * t + h4;
-      w2b[t] = P[po.W2 + k * H + row0 + l15];
-      wab[t] = P[po.Wa + k * H + row0 + l15];
-      wcb[t] = P[po.Wc + k * H + row0 + l15];
+      const int o = k * kStageRow + row0 + l15;
+      w2b[t] = stg[o];
+      wab[t] = stg[H * kStageRow + o];
+      wcb[t] = stg[2 * H * kStageRow + o];
     }
     f32x4 gW1[2], gW2[4], gWa[4], gWc[4];
 #pragma unroll
@@ -999,20 +1068,22 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
     }
 
     // ---- epilogue (backward team): each wave owns distinct rows of dW1, dW2, dWa, dWc, b1, b2
+    zero_image(img, nimg4, tid);
+    __syncthreads();  // (Z) pairs with the forward team's
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = row0 + 4 * h4 + r;
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib) {
         const int i = 16 * ib + l15;
-        slab_put(slab + (po.W2 + o * H + i), gW2[ib][r]);
-        slab_put(slab + (po.Wa + o * H + i), gWa[ib][r]);
-        slab_put(slab + (po.Wc + o * H + i), gWc[ib][r]);
+        img[po.W2 + o * H + i] = gW2[ib][r];
+        img[po.Wa + o * H + i] = gWa[ib][r];
+        img[po.Wc + o * H + i] = gWc[ib][r];
       }
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) {
         const int i = 16 * ib + l15;
-        if (i < a.D) slab_put(slab + (po.W1 + o * a.D + i), gW1[ib][r]);
+        if (i < a.D) img[po.W1 + o * a.D + i] = gW1[ib][r];
       }
       float v1 = gb1[r], v2 = gb2[r];
 #pragma unroll
@@ -1021,12 +1092,22 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
         v2 += __shfl_xor(v2, off);
       }
       if (l15 == 0) {
-        slab_put(slab + (po.b1 + o), v1);
-        slab_put(slab + (po.b2 + o), v2);
+        img[po.b1 + o] = v1;
+        img[po.b2 + o] = v2;
       }
     }
-    __syncthreads();  // pairs with the forward team's head-partial rendezvous
+    __syncthreads();  // (R) pairs with the forward team's head-partial rendezvous
   }
+  // the assembled slab leaves as 16-B write-through stores: ~13 MB per launch over the whole chip
+  // while the kernel drains, instead of 4-B pieces or dirty lines at the kernel boundary
+  __syncthreads();
+  for (int c = tid; c < nimg4; c += kThreads) slab_put4(slab + 4 * c, ((const f32x4*)img)[c]);
+#ifdef DPPO_PHASE_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  EDGE_STAMP(3);
+  EDGE_REAL(5);
+#endif
   if (a.fuse) fused_reduce_adam(a, lds_);
 }
 
@@ -1035,6 +1116,11 @@ __global__ __launch_bounds__(kThreads, 1) void mb_kernel(MArgs a) {
 #ifdef DPPO_PHASE_TRACE
 extern "C" __attribute__((visibility("default"))) int dppo_debug_phase_trace(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_trace), sizeof(g_phase_trace)) == hipSuccess
+             ? 0
+             : -2;
+}
+extern "C" __attribute__((visibility("default"))) int dppo_debug_phase_edges(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase_edges), sizeof(g_phase_edges)) == hipSuccess
              ? 0
              : -2;
 }
@@ -1047,7 +1133,9 @@ extern "C" __attribute__((visibility("default"))) int dppo_debug_heads_trace(lon
 
 size_t mb_lds_bytes(const MlpShape& sh) {
   const int D16 = (sh.D + 15) / 16 * 16;
-  return (size_t)make_lds2(D16).total * sizeof(float);
+  const Lds2 L = make_lds2(D16);
+  const int stage = L.H1[0] + kStageFloats;  // prologue weight staging over the step images
+  return (size_t)(L.total > stage ? L.total : stage) * sizeof(float);
 }
 
 int mb_grid(int32_t m) {
@@ -1087,8 +1175,11 @@ int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, in
     k.nblk = (int)((ga.p_total + 8 + kTailParams - 1) / kTailParams);
   }
   size_t lds = (size_t)k.L.total * sizeof(float);
-  // the epilogue reuses the step images: team-1 accumulators + per-wave head partials
-  const size_t epi = (size_t)(kTeamWaves * (16 + 3) * 64) * sizeof(float);  // head partials
+  // the prologue stages W2 | Wa | Wc over the step images; the epilogue reuses them for the
+  // per-wave head partials and the workgroup's slab image
+  const size_t stage = (size_t)(k.L.H1[0] + kStageFloats) * sizeof(float);
+  const size_t epi = (size_t)(kEpiHead + (ga.p_total + 8 + 3) / 4 * 4) * sizeof(float);
+  if (stage > lds) lds = stage;
   if (epi > lds) lds = epi;
   if (lds > 160 * 1024) {
     set_error("fused minibatch kernel needs %zu bytes of LDS (> 160 KiB)", lds);

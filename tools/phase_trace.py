@@ -76,8 +76,26 @@ def main():
         sp = span[ks].mean()
         tot += sp
         print(f"{i:>3} {NAMES0[i]:>22} {w0:8.0f} {NAMES1[i]:>10} {w1:8.0f} {sp:9.0f}")
+    print("per-wave phase cycles (waves 0-3 forward team, 4-7 backward team):")
+    for i in range(NI):
+        ks = [k for k in steady if k % NI == i]
+        print(f"  int {i}: " + " ".join(f"{work[ks][:, w].mean():6.0f}" for w in range(8)))
     print(f"set total {tot:.0f} cycles; whole launch {rel[nbar - 1].max() - rel[0].min():.0f} "
           f"cycles from first to last barrier")
+    if hasattr(h.lib, "dppo_debug_phase_edges"):
+        ed = np.zeros((256, 6), np.int64)
+        f3 = h.lib.dppo_debug_phase_edges
+        f3.argtypes = [ctypes.c_void_p]
+        assert f3(ed.ctypes.data) == 0
+        g = min(256, (mb + 31) // 32)
+        ed = ed[:g]
+        pro, loop, epi = ed[:, 1] - ed[:, 0], ed[:, 2] - ed[:, 1], ed[:, 3] - ed[:, 2]
+        rt0, rt1 = ed[:, 4], ed[:, 5]
+        print(f"workgroups {g}: prologue {np.median(pro):.0f} cycles (max {pro.max()}), main loop "
+              f"{np.median(loop):.0f} (max {loop.max()}), epilogue {np.median(epi):.0f} "
+              f"(max {epi.max()}); start skew {(rt0.max() - rt0.min()) / 100:.2f} us, end skew "
+              f"{(rt1.max() - rt1.min()) / 100:.2f} us, first start -> last end "
+              f"{(rt1.max() - rt0.min()) / 100:.2f} us (s_memrealtime)")
     if hasattr(h.lib, "dppo_debug_heads_trace"):
         hb = np.zeros((128, 4), np.int64)
         f2 = h.lib.dppo_debug_heads_trace
