@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/prof
 mkdir -p $OUT
 cd /tmp
 export TMPDIR=/tmp
-B="$R/bench.py --no-cpu-baseline --no-gae-roofline ${BENCH_ARGS}"
+B="$R/bench.py --no-cpu-baseline --no-gae-roofline --no-extra ${BENCH_ARGS}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
   python3 $B --steps 10 --warmup 2 > $OUT/kt.log 2>&1
 echo "kernel trace done"

@@ -27,7 +27,8 @@ CLASS = {"mb_kernel": "grad", "grad_kernel": "grad", "eval_kernel": "eval", "gae
          "pack_kernel": "pack", "slab_reduce_kernel": "slab_reduce",
          "clip_adam_kernel": "clip_adam", "reduce_adam_kernel": "reduce_adam",
          "stats_reduce_kernel": "adv_stats", "fy_build_kernel": "perm",
-         "fy_links_kernel": "perm", "fy_solve_kernel": "perm"}
+         "fy_links_kernel": "perm", "fy_solve_kernel": "perm", "shard_count_kernel": "perm",
+         "shard_write_kernel": "perm"}
 
 
 def short(name: str) -> str:
