@@ -474,7 +474,7 @@ int minibatch_grad(dppo_handle* h, const float* params, const int32_t* idx, cons
   ga.p_total = h->layout.total;
   // with `seg` the size is known only on the device: the handle's grid (sized for the largest
   // share a rank can hold) -- workgroups past the last step contribute zero slabs
-  int G = seg ? h->G : mb_grid(m);
+  int G = seg ? h->G : mb_grid(h->sh, m);
   if (G > h->G) G = h->G;
   {
     Timed tm(h, K_GRAD, s);
@@ -601,14 +601,14 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
         ga.slabs = h->slabs;
         ga.slab_stride = h->slab_stride;
         ga.p_total = h->layout.total;
-        int G = mb_grid(mb);
+        const bool fused_tail = std::getenv("DPPO_FUSED_ADAM") != nullptr;
+        int G = mb_grid(h->sh, mb, fused_tail);
         if (G > h->G) G = h->G;
         // DPPO_FUSED_ADAM=1: the slab reduction, clip and Adam as the minibatch kernel's own
         // tail (one launch per minibatch, two grid fan-ins).  Measured: the tail costs what
         // reduce_adam_kernel does (~8 us: the fan-ins, not the launch, dominate), throughput
         // within ~1.5 %; the separate kernel stays the default (and keeps the minibatch kernel's
         // roofline its own).
-        const bool fused_tail = std::getenv("DPPO_FUSED_ADAM") != nullptr;
         if (fused_tail) {
           FusedAdam fa{};
           fa.grad = h->grad;
@@ -725,8 +725,12 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
     cus = 256;
   h->num_cus = cus;
   // global minibatches: a rank's share of one varies around mb; size the grid for a whole one
-  h->G = mb_grid(h->gmb ? (int32_t)std::min<int64_t>(h->Bg / dims->num_minibatches, h->B)
-                        : (h->mb > 0 ? h->mb : 1));
+  // (the larger of the two kernels' grids: DPPO_FUSED_ADAM runs the two-team kernel)
+  {
+    const int32_t mg = h->gmb ? (int32_t)std::min<int64_t>(h->Bg / dims->num_minibatches, h->B)
+                              : (h->mb > 0 ? h->mb : 1);
+    h->G = std::max(mb_grid(h->sh, mg), mb_grid(h->sh, mg, true));
+  }
   if (h->G > cus) h->G = cus;
   h->slab_stride = round_up(h->layout.total + 8, 64);
   const int64_t E = dims->num_epochs, M = dims->num_minibatches;

@@ -224,11 +224,19 @@ struct FusedAdam {
   int ls_n;
   int add_entropy_const;
 };
-// Feature-split fused minibatch kernel (mbstep.hip), the one learn() uses.
+// Fused minibatch kernels.  launch_mb runs the sample-split kernel (mbwave.hip: one wave per
+// SIMD, heads on VALU, up to 4 actions) where it applies and the feature-split two-team kernel
+// (mbstep.hip) otherwise -- more actions, the fused Adam tail, or DPPO_MB_LEGACY=1.  mb_grid
+// gives the workgroup count (= gradient slabs) of the kernel launch_mb will run.
 size_t mb_lds_bytes(const MlpShape& sh);
-int mb_grid(int32_t m);
+int mb_grid(const MlpShape& sh, int32_t m, bool fused = false);
 int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
               hipStream_t s, const FusedAdam* fused = nullptr);
+bool mbw_supported(const MlpShape& sh);
+int mbw_grid(int32_t m);
+size_t mbw_lds_bytes(const MlpShape& sh);
+int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& a, int G,
+               hipStream_t s);
 
 // Optimiser kernels: optim.hip.
 int slab_reduce_blocks(int64_t p_total);

@@ -1138,7 +1138,8 @@ size_t mb_lds_bytes(const MlpShape& sh) {
   return (size_t)(L.total > stage ? L.total : stage) * sizeof(float);
 }
 
-int mb_grid(int32_t m) {
+int mb_grid(const MlpShape& sh, int32_t m, bool fused) {
+  if (!fused && mbw_supported(sh)) return mbw_grid(m);
   const int nsteps = (m + S - 1) / S;
   int g = nsteps;
   if (g > 256) g = 256;
@@ -1148,6 +1149,7 @@ int mb_grid(int32_t m) {
 
 int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, int G,
               hipStream_t s, const FusedAdam* fused) {
+  if (!fused && mbw_supported(sh)) return launch_mbw(sh, po, ga, G, s);
   MArgs k{};
   const int D16 = (sh.D + 15) / 16 * 16;
   k.L = make_lds2(D16);

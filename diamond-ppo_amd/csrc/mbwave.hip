@@ -1,0 +1,856 @@
+// Fused PPO minibatch step, sample-split form: one wave per SIMD, and each wave runs the whole
+// gather -> forward -> loss -> analytic backward -> weight-gradient accumulation of its own
+// 16-sample groups with every activation in registers.  No workgroup barrier inside the main
+// loop: the only cross-wave step is the final sum of the four waves' gradients.
+//
+// Reference: loss and backward of one minibatch, diamond/ppo.py:261-283 (continuous:
+// continuous_ppo.py:273-295), default networks ppo.py:53-71 / continuous_ppo.py:63-81.
+//
+// ---- Register layouts (lane l = 16 q + r of a wave) --------------------------------------------
+// v_mfma_f32_16x16x4_f32 takes A[i][k] from lane (q = k, r = i), B[k][j] from lane (k, j) and
+// leaves D[4q + v][r] in register v of lane (q, r).
+// * N layout of a [64 features x 16 samples] activation, four f32x4 tiles b: register v of tile b
+//   in lane (q, r) = feature 16b + 4q + v of sample r.  It is what the forward produces (A =
+//   weight rows, B = input) and, read as B with k-step (b, v) <-> features {16b + 4q + v}, what
+//   the next layer consumes: the forward chains in registers.
+// * T layout: register v of tile b in lane (q, r) = feature 16b + r of sample 4q + v.  The
+//   backward produces it (A = dZ in N layout, i.e. i = sample, B = W) and the weight gradient
+//   dW += dZ X^T takes both operands in it (k = sample, k-step v <-> samples {4q + v}).
+// Each layer therefore needs its input activation and its output delta in both layouts; the
+// N -> T / T -> N turns go through a wave-private LDS scratch (b128 one way, b32 the other,
+// conflict-free strides 68 / 72).
+//
+// ---- LDS ------------------------------------------------------------------------------------------
+// The hidden weights W2, Wa, Wc stay in LDS for the launch (read-only), rows padded to 68 floats:
+// the forward's row-slice ds_read_b128 (lane (q, r): row 16ob + r, floats 16kb + 4q ..) and the
+// backward's column ds_read_b32 (lane (q, r): row 16ob + 4q + v, column 16rb + r) both address
+// one base register per lane plus compile-time offsets (the layout is constexpr), and are
+// conflict-free (b32) / one 2-way pair per 16-lane group (b128).
+//
+// Heads (at most 4 actions) and the per-sample loss run on VALU in the N layout: each lane dots
+// the 16 head-input features it holds, the four lanes of a sample (q = 0..3) are summed with
+// v_permlane16/32_swap, and every lane then has its sample's logits / mean and value.
+//
+// Every partial sum is reduced in a fixed order and written once per workgroup into its gradient
+// slab (optim.hip sums the slabs in a fixed order): bit-reproducible, no float atomics.
+#include "common.h"
+
+namespace dppo {
+namespace {
+
+constexpr int H = 64;
+constexpr int kWavesW = 4;                  // one wave per SIMD
+constexpr int kThreadsW = kWavesW * kWave;  // 256
+constexpr int kSmN = 68;                    // N -> T scratch: [16 samples][68]
+constexpr int kSmT = 72;                    // T -> N scratch: [16 samples][72]
+constexpr int kSlot = 16 * kSmT;                      // one turn slot (either stride)
+constexpr int kScratch = 4 * kSlot + 16 * 8;          // floats per wave: 4 slots + head deltas
+constexpr int kMat = H * H;                 // one hidden weight matrix
+constexpr float kLogSqrt2PiW = 0.91893853320467274178f;
+constexpr float kLn2W = 0.69314718055994530942f;
+constexpr float kHalfLog2PiPlusHalfW = 1.41893853320467274178f;
+
+// Scheduling fence between the phases of a group: keeps the compiler from hoisting one phase's
+// LDS / global loads into the previous one (which raises register pressure past the budget of
+// one wave per SIMD: 208 accumulator + ~230 working registers).
+#define PHASE_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+#ifdef DPPO_PHASE_TRACE
+// per workgroup: s_memtime at entry, main-loop entry, main-loop exit, end; s_memrealtime at entry
+// and at the end (in-kernel clock, cross-CU skew)
+__device__ long long g_mbw_edges[256][6];
+#define WEDGE(i, v)                                                     \
+  do {                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_mbw_edges[blockIdx.x][i] = (v); \
+  } while (0)
+#else
+#define WEDGE(i, v) \
+  do {              \
+  } while (0)
+#endif
+
+constexpr int kWS = 68;  // row stride of the hidden weight images
+
+struct WLds {   // offsets in floats (compile-time: one layout per input width)
+  int W2;       // W2 | Wa | Wc: [3][64][kWS]
+  int scratch;  // [4 waves][kScratch]
+  int Wo, Wv;   // [4][64] (rows >= A zero), [64]
+  int b1, b2, ba, bc;
+  int bo, bv, ls;  // [4] each
+  int gc;       // [4][4]: 1/(2 var), 1/var, 1/sigma, log sigma per action (continuous)
+  int gent;     // [4]: {sum entropy terms, sum log-prob constants}
+  int W1, RS1;  // W1 [64][RS1]
+  int total;
+};
+
+struct WArgs {
+  ParamOffsets po;
+  const float* params;
+  const float* rec;
+  const int32_t* idx;
+  const int32_t* seg;  // global-minibatch DP: {start, end} of this minibatch in idx (device)
+  int m;
+  float inv_m, clip_eps, vf, ent;
+  float* slabs;
+  int64_t slab_stride, p_total;
+  int D, D8, A, R, nkn;
+};
+
+constexpr WLds make_wlds(int D16) {
+  WLds L{};
+  int o = 0;
+  L.W2 = o;
+  o += 3 * H * kWS;
+  L.scratch = o;
+  o += kWavesW * kScratch;
+  L.Wo = o;
+  o += 4 * H;
+  L.Wv = o;
+  o += H;
+  L.b1 = o;
+  o += H;
+  L.b2 = o;
+  o += H;
+  L.ba = o;
+  o += H;
+  L.bc = o;
+  o += H;
+  L.bo = o;
+  o += 4;
+  L.bv = o;
+  o += 4;
+  L.ls = o;
+  o += 4;
+  L.gc = o;
+  o += 16;
+  L.gent = o;
+  o += 4;
+  L.W1 = o;
+  L.RS1 = D16 + 2;
+  o += H * L.RS1;
+  L.total = (o + 3) & ~3;
+  return L;
+}
+
+// Epilogue staging: two [4 waves][64 x 64] buffers, then the small per-wave items.
+constexpr int kSmallW = 4 * H + 5 * H + 16;  // biases | Wo rows (<= 4) | Wv | scalars
+constexpr int kEpiFloats = 2 * kWavesW * kMat + kWavesW * kSmallW;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float tanh_w(float x) {
+  // t = e^{-2|x|}, tanh = sign(x) (1 - t) / (1 + t): one exp, one hardware reciprocal
+  const float t = __expf(-2.0f * fabsf(x));
+  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
+}
+
+__device__ __forceinline__ void tanh4(f32x4 (&y)[4]) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) y[b][v] = tanh_w(y[b][v]);
+}
+
+// Sum over the four lanes of a sample (q = 0..3, same r): rows 0+1 and 2+3 with
+// v_permlane16_swap, then the two halves with v_permlane32_swap.  The same additions in the same
+// order in every lane.
+__device__ __forceinline__ float qsum(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  const float s = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  const auto p2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false,
+                                                   false);
+  return __uint_as_float(p2[0]) + __uint_as_float(p2[1]);
+}
+
+__device__ __forceinline__ float dot4(f32x4 w, f32x4 x) {
+  return (w[0] * x[0] + w[1] * x[1]) + (w[2] * x[2] + w[3] * x[3]);
+}
+
+// Forward of one hidden layer, N -> N: y[ob] += W[16ob + i][:] x for the four 16-row output
+// blocks; the A operand of k-steps (kb, 0..3) is one ds_read_b128 of the row.
+__device__ __forceinline__ void fwd64(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4], int q,
+                                      int r) {
+  f32x4 w[2][4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) w[0][ob] = *(const f32x4*)(W + (16 * ob + r) * kWS + 4 * q);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    if (kb + 1 < 4) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+        w[(kb + 1) & 1][ob] = *(const f32x4*)(W + (16 * ob + r) * kWS + 16 * (kb + 1) + 4 * q);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) y[ob] = mfma4(w[kb & 1][ob][v], x[kb][v], y[ob]);
+  }
+}
+
+// Two layers on the same input (actor / critic hidden): eight independent accumulation chains.
+__device__ __forceinline__ void fwd64x2(f32x4 (&y)[4], const float* W, f32x4 (&z)[4],
+                                        const float* U, const f32x4 (&x)[4], int q, int r) {
+  f32x4 w[2][4], u[2][4];
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) {
+    const int o = (16 * ob + r) * kWS + 4 * q;
+    w[0][ob] = *(const f32x4*)(W + o);
+    u[0][ob] = *(const f32x4*)(U + o);
+  }
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    if (kb + 1 < 4) {
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        const int o = (16 * ob + r) * kWS + 16 * (kb + 1) + 4 * q;
+        w[(kb + 1) & 1][ob] = *(const f32x4*)(W + o);
+        u[(kb + 1) & 1][ob] = *(const f32x4*)(U + o);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) {
+        y[ob] = mfma4(w[kb & 1][ob][v], x[kb][v], y[ob]);
+        z[ob] = mfma4(u[kb & 1][ob][v], x[kb][v], z[ob]);
+      }
+  }
+}
+
+// Backward through one hidden layer into the T layout: t[rb] += sum_out dz[out][s] W[out][16rb+c]
+// (A = dz in N layout, B = a column piece of W: ds_read_b32).
+__device__ __forceinline__ void bwdT(f32x4 (&t)[4], const float* W, const f32x4 (&dz)[4], int q,
+                                     int r) {
+  float b[2][4];
+  auto ld = [&](int k, int slot) {
+    const int R = 16 * (k >> 2) + 4 * q + (k & 3);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) b[slot][rb] = W[R * kWS + 16 * rb + r];
+  };
+  ld(0, 0);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k + 1 < 16) ld(k + 1, (k + 1) & 1);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) t[rb] = mfma4(dz[k >> 2][k & 3], b[k & 1][rb], t[rb]);
+  }
+}
+
+// dW[16ob.., 16ib..] += dZ X^T over the group's 16 samples (both operands in T layout).
+template <int NIB>
+__device__ __forceinline__ void wgrad(f32x4* acc, const f32x4 (&dzt)[4], const f32x4* xt) {
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int ib = 0; ib < NIB; ++ib)
+        acc[ob * NIB + ib] = mfma4(dzt[ob][v], xt[ib][v], acc[ob * NIB + ib]);
+}
+
+// N -> T through the wave's scratch (sample-major rows of 68 floats).
+__device__ __forceinline__ void put_n(float* sm, const f32x4 (&n)[4], int q, int r) {
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) *(f32x4*)(sm + r * kSmN + 16 * ob + 4 * q) = n[ob];
+}
+__device__ __forceinline__ void get_t(f32x4 (&t)[4], const float* sm, int q, int r) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) t[b][v] = sm[(4 * q + v) * kSmN + 16 * b + r];
+}
+// T -> N (rows of 72 floats).
+__device__ __forceinline__ void put_t(float* sm, const f32x4 (&t)[4], int q, int r) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) sm[(4 * q + v) * kSmT + 16 * b + r] = t[b][v];
+}
+__device__ __forceinline__ void get_n(f32x4 (&n)[4], const float* sm, int q, int r) {
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) n[ob] = *(const f32x4*)(sm + r * kSmT + 16 * ob + 4 * q);
+}
+
+__device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ f32x4 z4() { return (f32x4){0.f, 0.f, 0.f, 0.f}; }
+
+// One group's sample indices: the lane's own sample (N layout) and the four of the T layout.
+struct Fetch {
+  int sn, st[4];
+};
+// One group's record data.
+template <int NIB>
+struct GRec {
+  float xn[4 * NIB];  // layer-1 B operand: input 4t + q of sample r
+  f32x4 xt[NIB];      // T layout of the input: feature 16ib + r of samples 4q + v
+  f32x4 sc;           // {action bits, old log-prob, advantage, return} of sample r
+  f32x4 ca;           // continuous action of sample r (<= 4 dims)
+};
+
+template <int AMAX, bool CONT, int NIB>
+__global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+#ifdef DPPO_PHASE_TRACE
+  WEDGE(0, (long long)__builtin_amdgcn_s_memtime());
+  WEDGE(4, (long long)__builtin_amdgcn_s_memrealtime());
+#endif
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, r = lane & 15;
+  constexpr WLds L = make_wlds(16 * NIB);
+  const float* P = a.params;
+  const ParamOffsets& po = a.po;
+  int mm = a.m;
+  const int32_t* idxp = a.idx;
+  if (a.seg) {  // this rank's share of a global minibatch is known only on the device
+    const int s0 = a.seg[0];
+    mm = a.seg[1] - s0;
+    idxp += s0;
+  }
+  const int ngroups = (mm + 15) >> 4;
+  const int first = (int)blockIdx.x * kWavesW + wave;  // group k of this wave: first + k * stride
+  const int stride = (int)gridDim.x * kWavesW;
+  const int nk = first < ngroups ? (ngroups - first + stride - 1) / stride : 0;
+  const int R = a.R, D = a.D;
+
+  // Loads never branch: out-of-range positions read a valid address and are zeroed after.
+  auto fetch = [&](int k) {
+    Fetch f;
+    const int g0 = (first + k * stride) * 16;
+    const int sn = g0 + r;
+    f.sn = idxp[sn < mm ? sn : mm - 1];
+    if (sn >= mm) f.sn = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int st = g0 + 4 * q + v;
+      f.st[v] = idxp[st < mm ? st : mm - 1];
+      if (st >= mm) f.st[v] = 0;
+    }
+    return f;
+  };
+  auto gather = [&](const Fetch& f) {
+    GRec<NIB> g;
+    const float* rn = a.rec + (int64_t)f.sn * R;
+#pragma unroll
+    for (int t = 0; t < 4 * NIB; ++t) {
+      const int c = 4 * t + q;
+      const float x = rn[c < D ? c : D - 1];
+      g.xn[t] = c < D ? x : 0.0f;
+    }
+#pragma unroll
+    for (int ib = 0; ib < NIB; ++ib)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int c = 16 * ib + r;
+        const float x = a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
+        g.xt[ib][v] = c < D ? x : 0.0f;
+      }
+    g.sc = *(const f32x4*)(rn + a.D8);
+    g.ca = CONT ? *(const f32x4*)(rn + a.D8 + 4) : z4();
+    return g;
+  };
+
+  // the first groups' indices go out before the weight staging (their gathers wait on them)
+  Fetch f_cur{}, f_nxt{};
+  if (nk > 0) f_cur = fetch(0);
+  if (nk > 1) f_nxt = fetch(1);
+
+  // ---------------- prologue: weights into LDS
+  for (int k = tid; k < 3 * (kMat / 4); k += kThreadsW) {
+    const int mi = k >> 10, e = k & 1023, row = e >> 4, g = e & 15;
+    const int64_t off = mi == 0 ? po.W2 : (mi == 1 ? po.Wa : po.Wc);
+    const f32x4 v = *(const f32x4*)(P + off + row * H + 4 * g);
+    *(f32x4*)(lds + L.W2 + mi * H * kWS + row * kWS + 4 * g) = v;
+  }
+  for (int k = tid; k < H * L.RS1; k += kThreadsW) {
+    const int row = k / L.RS1, c = k - row * L.RS1;
+    lds[L.W1 + k] = c < D ? P[po.W1 + row * D + c] : 0.0f;
+  }
+  for (int k = tid; k < 4 * H; k += kThreadsW) {
+    const int h = k >> 6;
+    lds[L.Wo + k] = h < a.A ? P[po.Wo + k] : 0.0f;
+  }
+  if (tid < H) {
+    lds[L.Wv + tid] = P[po.Wv + tid];
+    lds[L.b1 + tid] = P[po.b1 + tid];
+    lds[L.b2 + tid] = P[po.b2 + tid];
+    lds[L.ba + tid] = P[po.ba + tid];
+    lds[L.bc + tid] = P[po.bc + tid];
+  } else if (tid < H + 4) {
+    const int h = tid - H;
+    lds[L.bo + h] = h < a.A ? P[po.bo + h] : 0.0f;
+    lds[L.ls + h] = (CONT && h < a.A) ? P[po.ls + h] : 0.0f;
+    lds[L.bv + h] = h == 0 ? P[po.bv] : 0.0f;
+    if (CONT) {
+      // Normal(mean, exp(log_std)) constants of action h (continuous_ppo.py:41-47; torch
+      // Normal.log_prob / entropy), the same for every sample
+      const bool on = h < a.A;
+      const float sg = on ? __expf(P[po.ls + h]) : 1.0f;
+      lds[L.gc + h] = on ? 1.0f / (2.0f * (sg * sg)) : 0.0f;
+      lds[L.gc + 4 + h] = 1.0f / (sg * sg);
+      lds[L.gc + 8 + h] = 1.0f / sg;
+      lds[L.gc + 12 + h] = on ? __logf(sg) : 0.0f;
+      if (h == 0) {
+        float e = 0.0f, c = 0.0f;
+        for (int k = 0; k < a.A && k < 4; ++k) {
+          const float l = __logf(__expf(P[po.ls + k]));
+          e += kHalfLog2PiPlusHalfW + l;  // entropy (continuous_ppo.py:45-47)
+          c += l + kLogSqrt2PiW;           // log-prob constant part
+        }
+        lds[L.gent] = e;
+        lds[L.gent + 1] = c;
+      }
+    }
+  }
+  GRec<NIB> g_cur{};
+  if (nk > 0) g_cur = gather(f_cur);
+  __syncthreads();
+
+  const float* W2 = lds + L.W2;
+  const float* Wa = W2 + H * kWS;
+  const float* Wc = W2 + 2 * H * kWS;
+  // the wave's scratch: four [16 x 72] turn slots and the per-sample head-delta image [16][8]
+  float* sh1 = lds + L.scratch + wave * kScratch;  // h1 (N -> T), read back for dW2 / dz1
+  float* sh2 = sh1 + kSlot;                         // h2 (N -> T), read back for dWa, dWc / dz2
+  float* sx = sh2 + kSlot;                          // a1 (N -> T), then dza, then dz2 (T -> N)
+  float* sy = sx + kSlot;                           // c1 (N -> T), then dzc
+  float* sd = sy + kSlot;                           // {dlogit[0..3], dvalue} per sample
+
+  f32x4 gW2[16], gWa[16], gWc[16], gW1[4 * NIB];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gW2[i] = gWa[i] = gWc[i] = z4();
+#pragma unroll
+  for (int i = 0; i < 4 * NIB; ++i) gW1[i] = z4();
+  // T-form partials (component b = feature 16b + r, summed over this lane's samples 4q + v)
+  f32x4 gb1 = z4(), gb2 = z4(), gba = z4(), gbc = z4(), gWv = z4();
+  f32x4 gWo[AMAX];
+#pragma unroll
+  for (int h = 0; h < AMAX; ++h) gWo[h] = z4();
+  float gbo[AMAX], gls[AMAX], gbv = 0.f, s_pi = 0.f, s_v = 0.f, s_ent = 0.f;
+#pragma unroll
+  for (int h = 0; h < AMAX; ++h) gbo[h] = gls[h] = 0.f;
+#ifdef DPPO_PHASE_TRACE
+  WEDGE(1, (long long)__builtin_amdgcn_s_memtime());
+#endif
+
+  for (int k = 0; k < nk; ++k) {
+    const int g0 = (first + k * stride) * 16;
+    const bool valid = g0 + r < mm;
+    // ---- (1) layer 1: h1 = tanh(W1 x + b1); k-step t covers inputs {4t + q}
+    f32x4 h1[4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) h1[ob] = *(const f32x4*)(lds + L.b1 + 16 * ob + 4 * q);
+#pragma unroll
+    for (int t = 0; t < 4 * NIB; ++t) {
+      if (t < a.nkn) {
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+          h1[ob] = mfma4(lds[L.W1 + (16 * ob + r) * L.RS1 + 4 * t + q], g_cur.xn[t], h1[ob]);
+      }
+    }
+    tanh4(h1);
+    put_n(sh1, h1, q, r);
+    PHASE_FENCE();
+    // ---- (2) layer 2
+    f32x4 h2[4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) h2[ob] = *(const f32x4*)(lds + L.b2 + 16 * ob + 4 * q);
+    fwd64(h2, W2, h1, q, r);
+    tanh4(h2);
+    put_n(sh2, h2, q, r);
+    PHASE_FENCE();
+    // ---- (3) actor / critic hidden layers
+    f32x4 a1[4], c1[4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      a1[ob] = *(const f32x4*)(lds + L.ba + 16 * ob + 4 * q);
+      c1[ob] = *(const f32x4*)(lds + L.bc + 16 * ob + 4 * q);
+    }
+    fwd64x2(a1, Wa, c1, Wc, h2, q, r);
+    tanh4(a1);
+    tanh4(c1);
+    put_n(sx, a1, q, r);
+    put_n(sy, c1, q, r);
+    PHASE_FENCE();
+    // ---- (4) heads: logits / means and value of sample r, in every lane of the sample
+    float out[AMAX];
+#pragma unroll
+    for (int h = 0; h < AMAX; ++h) {
+      float s = 0.f;
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+        s += dot4(*(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q), a1[ob]);
+      out[h] = qsum(s) + lds[L.bo + h];
+    }
+    float vpart = 0.f;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+      vpart += dot4(*(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q), c1[ob]);
+    const float val = qsum(vpart) + lds[L.bv];
+    // ---- (5) per-sample loss and head deltas (ppo.py:264-280)
+    const f32x4 sc = g_cur.sc;
+    const float adv = sc[2], ret = sc[3];
+    float logp = 0.f, ent = 0.f;
+    float p[AMAX], lp[AMAX];
+    if (CONT) {
+      float qq = 0.f;
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h) {
+        const float d = g_cur.ca[h] - out[h];
+        qq += (d * d) * lds[L.gc + h];  // 1 / (2 var): 0 past A
+      }
+      logp = -qq - lds[L.gent + 1];
+      ent = lds[L.gent];
+    } else {
+      const int actn = __float_as_int(sc[0]);
+      float mx = out[0];
+#pragma unroll
+      for (int h = 1; h < AMAX; ++h)
+        if (h < a.A) mx = fmaxf(mx, out[h]);
+      float se = 0.f;
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h)
+        if (h < a.A) se += __expf(out[h] - mx);
+      // se >= 1 (its largest term is exp(0)): the bare v_log_f32 (log2) needs no range fix-up
+      const float lse = mx + __builtin_amdgcn_logf(se) * kLn2W;
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h) {
+        lp[h] = out[h] - lse;
+        p[h] = h < a.A ? __expf(lp[h]) : 0.f;
+        ent -= p[h] * lp[h];
+        logp = h == actn ? lp[h] : logp;
+      }
+    }
+    const float ratio = __expf(logp - sc[1]);                      // ppo.py:266
+    const float rcl = fminf(fmaxf(ratio, 1.0f - a.clip_eps), 1.0f + a.clip_eps);
+    const float u = -adv * ratio, w = -adv * rcl;                  // ppo.py:267-269
+    const float inr = (ratio >= 1.0f - a.clip_eps && ratio <= 1.0f + a.clip_eps) ? 1.f : 0.f;
+    const float gu = u > w ? 1.f : (u == w ? 0.5f : 0.f);          // torch.max splits ties
+    const float gw = w > u ? 1.f : (u == w ? 0.5f : 0.f);
+    const float vm = valid ? a.inv_m : 0.f;
+    const float dlogp = (gu * -adv + gw * -adv * inr) * vm * ratio;
+    const float dv = a.vf * (val - ret) * vm;                       // ppo.py:272
+    float dl[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < AMAX; ++h) {
+      if (CONT) {
+        const float dd = g_cur.ca[h] - out[h];
+        const float zz = dd * lds[L.gc + 8 + h];
+        dl[h] = h < a.A ? dlogp * dd * lds[L.gc + 4 + h] : 0.f;
+        if (q == 0 && h < a.A) gls[h] += dlogp * (zz * zz - 1.0f);
+      } else {
+        const int actn = __float_as_int(sc[0]);
+        dl[h] = dlogp * ((h == actn ? 1.f : 0.f) - p[h]) + a.ent * vm * p[h] * (lp[h] + ent);
+      }
+    }
+    if (q == 0) {
+      if (valid) {
+        s_pi += fmaxf(u, w);
+        s_v += 0.5f * (val - ret) * (val - ret);
+        s_ent += ent;
+      }
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h) gbo[h] += dl[h];
+      gbv += dv;
+      *(f32x4*)(sd + 8 * r) = (f32x4){dl[0], dl[1], dl[2], dl[3]};
+      sd[8 * r + 4] = dv;
+    }
+    PHASE_FENCE();
+    // ---- (6) head weight gradients (T layout: feature 16cb + r, samples 4q + v), then the head
+    // back-propagation dza = (Wo^T dl)(1 - a1^2), dzc = Wv dv (1 - c1^2) in the N layout
+    {
+      f32x4 a1t[4], c1t[4];
+      get_t(a1t, sx, q, r);
+      get_t(c1t, sy, q, r);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const f32x4 d4 = *(const f32x4*)(sd + 8 * (4 * q + v));
+        const float dvs = sd[8 * (4 * q + v) + 4];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+#pragma unroll
+          for (int h = 0; h < AMAX; ++h) gWo[h][cb] += d4[h] * a1t[cb][v];
+          gWv[cb] += dvs * c1t[cb][v];
+        }
+      }
+    }
+    f32x4 dza[4], dzc[4];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) {
+      f32x4 da = z4();
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h)
+        da += *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q) * dl[h];
+      dza[ob] = da * (1.0f - a1[ob] * a1[ob]);
+      dzc[ob] = (*(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q) * dv) * (1.0f - c1[ob] * c1[ob]);
+    }
+    put_n(sx, dza, q, r);
+    put_n(sy, dzc, q, r);
+    PHASE_FENCE();
+    // ---- (7) dh2 = Wa^T dza + Wc^T dzc (T layout)
+    f32x4 dh2[4] = {z4(), z4(), z4(), z4()};
+    bwdT(dh2, Wa, dza, q, r);
+    bwdT(dh2, Wc, dzc, q, r);
+    // the next group's records (its indices came one group ago) and the indices after that
+    GRec<NIB> g_nxt{};
+    if (k + 1 < nk) g_nxt = gather(f_nxt);
+    if (k + 2 < nk) f_nxt = fetch(k + 2);
+    PHASE_FENCE();
+    // ---- (8) dz2 = dh2 (1 - h2^2); hidden-bias partials; dWa, dWc
+    {
+      f32x4 h2t[4], dzat[4], dzct[4], dz2t[4];
+      get_t(dzat, sx, q, r);
+      get_t(dzct, sy, q, r);
+      get_t(h2t, sh2, q, r);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        dz2t[b] = dh2[b] * (1.0f - h2t[b] * h2t[b]);
+        gba[b] += (dzat[b][0] + dzat[b][1]) + (dzat[b][2] + dzat[b][3]);
+        gbc[b] += (dzct[b][0] + dzct[b][1]) + (dzct[b][2] + dzct[b][3]);
+        gb2[b] += (dz2t[b][0] + dz2t[b][1]) + (dz2t[b][2] + dz2t[b][3]);
+      }
+      put_t(sx, dz2t, q, r);
+      wgrad<4>(gWa, dzat, h2t);
+      wgrad<4>(gWc, dzct, h2t);
+    }
+    PHASE_FENCE();
+    // ---- (9) dh1 = W2^T dz2 ; dz1 = dh1 (1 - h1^2) ; dW2 ; dW1
+    {
+      f32x4 dz2[4], dz2t[4], h1t[4];
+      get_n(dz2, sx, q, r);
+      f32x4 dh1[4] = {z4(), z4(), z4(), z4()};
+      bwdT(dh1, W2, dz2, q, r);
+      // dz2 again in the T layout (from the same slot) and h1 for dW2
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dz2t[b][v] = sx[(4 * q + v) * kSmT + 16 * b + r];
+      get_t(h1t, sh1, q, r);
+      wgrad<4>(gW2, dz2t, h1t);
+      f32x4 dz1t[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        dz1t[b] = dh1[b] * (1.0f - h1t[b] * h1t[b]);
+        gb1[b] += (dz1t[b][0] + dz1t[b][1]) + (dz1t[b][2] + dz1t[b][3]);
+      }
+      wgrad<NIB>(gW1, dz1t, g_cur.xt);
+    }
+    g_cur = g_nxt;
+    PHASE_FENCE();
+  }
+#ifdef DPPO_PHASE_TRACE
+  WEDGE(2, (long long)__builtin_amdgcn_s_memtime());
+#endif
+
+  // ---------------- epilogue: the four waves' partials summed in LDS in a fixed order
+  float* slab = a.slabs + (int64_t)blockIdx.x * a.slab_stride;
+  float* stg0 = lds;
+  float* stg1 = lds + kWavesW * kMat;
+  float* small = lds + 2 * kWavesW * kMat;
+  auto put_mat = [&](float* stg, const f32x4* acc, int nib, int cols) {
+    float* s = stg + wave * kMat;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+      for (int ib = 0; ib < nib; ++ib) {
+        const int col = 16 * ib + r;
+        if (col < cols) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) s[(16 * ob + 4 * q + v) * cols + col] = acc[ob * nib + ib][v];
+        }
+      }
+  };
+  auto sum_mat = [&](const float* stg, int64_t off, int n4) {
+    for (int c = tid; c < n4; c += kThreadsW) {
+      const f32x4 v = ((((const f32x4*)stg)[c] + ((const f32x4*)(stg + kMat))[c]) +
+                       ((const f32x4*)(stg + 2 * kMat))[c]) +
+                      ((const f32x4*)(stg + 3 * kMat))[c];
+      slab_st4(slab + off + 4 * c, v);
+    }
+  };
+  __syncthreads();  // every wave is done with the weights and its scratch
+  put_mat(stg0, gW2, 4, H);
+  put_mat(stg1, gWa, 4, H);
+  {
+    // small items of this wave: hidden biases and head weights (T form: reduce over q), head
+    // biases / log-std / loss sums (every lane)
+    float* s = small + wave * kSmallW;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float x1 = qsum(gb1[b]), x2 = qsum(gb2[b]), xa = qsum(gba[b]), xc = qsum(gbc[b]);
+      const float xv = qsum(gWv[b]);
+      float xo[AMAX];
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h) xo[h] = qsum(gWo[h][b]);
+      if (q == 0) {
+        const int f = 16 * b + r;
+        s[0 * H + f] = x1;
+        s[1 * H + f] = x2;
+        s[2 * H + f] = xa;
+        s[3 * H + f] = xc;
+#pragma unroll
+        for (int h = 0; h < AMAX; ++h) s[4 * H + h * H + f] = xo[h];
+        s[8 * H + f] = xv;
+      }
+    }
+    float sc[2 * AMAX + 4];
+#pragma unroll
+    for (int h = 0; h < AMAX; ++h) {
+      sc[h] = gbo[h];
+      sc[AMAX + h] = gls[h];
+    }
+    sc[2 * AMAX] = gbv;
+    sc[2 * AMAX + 1] = s_pi;
+    sc[2 * AMAX + 2] = s_v;
+    sc[2 * AMAX + 3] = s_ent;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < 2 * AMAX + 4; ++j) sc[j] += __shfl_xor(sc[j], off);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 2 * AMAX + 4; ++j) s[9 * H + j] = sc[j];
+    }
+  }
+  __syncthreads();
+  sum_mat(stg0, po.W2, kMat / 4);
+  sum_mat(stg1, po.Wa, kMat / 4);
+  for (int j = tid; j < kSmallW; j += kThreadsW) {
+    const float v = ((small[j] + small[kSmallW + j]) + small[2 * kSmallW + j]) +
+                    small[3 * kSmallW + j];
+    if (j < 4 * H) {
+      const int l = j >> 6, f = j & 63;
+      const int64_t off = l == 0 ? po.b1 : (l == 1 ? po.b2 : (l == 2 ? po.ba : po.bc));
+      slab[off + f] = v;
+    } else if (j < 8 * H) {
+      const int h = (j - 4 * H) >> 6, f = j & 63;
+      if (h < a.A && h < AMAX) slab[po.Wo + h * H + f] = v;
+    } else if (j < 9 * H) {
+      slab[po.Wv + (j - 8 * H)] = v;
+    } else {
+      const int e = j - 9 * H;
+      if (e < AMAX) {
+        if (e < a.A) slab[po.bo + e] = v;
+      } else if (e < 2 * AMAX) {
+        if (CONT && e - AMAX < a.A) slab[po.ls + (e - AMAX)] = v;
+      } else if (e == 2 * AMAX) {
+        slab[po.bv] = v;
+      } else if (e < 2 * AMAX + 4) {
+        slab[a.p_total + (e - 2 * AMAX - 1)] = v;
+      }
+    }
+  }
+  __syncthreads();  // stg0 / stg1 reused
+  put_mat(stg0, gWc, 4, H);
+  put_mat(stg1, gW1, NIB, D);
+  __syncthreads();
+  sum_mat(stg0, po.Wc, kMat / 4);
+  sum_mat(stg1, po.W1, H * D / 4);
+#ifdef DPPO_PHASE_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  WEDGE(3, (long long)__builtin_amdgcn_s_memtime());
+  WEDGE(5, (long long)__builtin_amdgcn_s_memrealtime());
+#endif
+}
+
+}  // namespace
+
+#ifdef DPPO_PHASE_TRACE
+extern "C" __attribute__((visibility("default"))) int dppo_debug_mbw_edges(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbw_edges), sizeof(g_mbw_edges)) == hipSuccess
+             ? 0
+             : -2;
+}
+#endif
+
+bool mbw_supported(const MlpShape& sh) {
+  static const int legacy = [] {
+    const char* e = std::getenv("DPPO_MB_LEGACY");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return !legacy && sh.A <= 4 && sh.D <= 32;
+}
+
+int mbw_grid(int32_t m) {
+  int g = (m + 63) / 64;  // 64 samples per workgroup round (4 waves x 16)
+  if (g > 256) g = 256;
+  if (g < 1) g = 1;
+  return g;
+}
+
+size_t mbw_lds_bytes(const MlpShape& sh) {
+  const int D16 = (sh.D + 15) / 16 * 16;
+  const WLds L = make_wlds(D16);
+  const int n = L.total > kEpiFloats ? L.total : kEpiFloats;
+  return (size_t)n * sizeof(float);
+}
+
+int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, int G,
+               hipStream_t s) {
+  WArgs k{};
+  const int D16 = (sh.D + 15) / 16 * 16;
+  k.po = po;
+  k.params = ga.params;
+  k.rec = ga.rec;
+  k.idx = ga.idx;
+  k.seg = ga.seg;
+  k.m = ga.m;
+  k.inv_m = ga.inv_m;
+  k.clip_eps = ga.clip_eps;
+  k.vf = ga.vf_coef;
+  k.ent = ga.ent_coef;
+  k.slabs = ga.slabs;
+  k.slab_stride = ga.slab_stride;
+  k.p_total = ga.p_total;
+  k.D = sh.D;
+  k.D8 = sh.D8;
+  k.A = sh.A;
+  k.R = sh.R;
+  k.nkn = (sh.D + 3) / 4;
+  const size_t lds = mbw_lds_bytes(sh);
+  if (lds > 160 * 1024) {
+    set_error("minibatch kernel needs %zu bytes of LDS (> 160 KiB)", lds);
+    return DPPO_EUNSUPPORTED;
+  }
+  static bool attr = false;
+  if (!attr) {
+    attr = true;
+#define DPPO_SETW(A, C, N)                                                                    \
+  (void)hipFuncSetAttribute((const void*)mbw_kernel<A, C, N>,                                 \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    DPPO_SETW(2, false, 1) DPPO_SETW(2, true, 1) DPPO_SETW(4, false, 1) DPPO_SETW(4, true, 1)
+    DPPO_SETW(2, false, 2) DPPO_SETW(2, true, 2) DPPO_SETW(4, false, 2) DPPO_SETW(4, true, 2)
+#undef DPPO_SETW
+  }
+  const dim3 grid((unsigned)G), block(kThreadsW);
+  const bool c = sh.continuous != 0;
+  const bool n2 = D16 > 16;
+#define DPPO_LW(A, C, N) DPPO_LAUNCH((mbw_kernel<A, C, N>), grid, block, lds, s, k)
+  if (sh.A <= 2) {
+    if (n2) {
+      if (c) DPPO_LW(2, true, 2);
+      else DPPO_LW(2, false, 2);
+    } else {
+      if (c) DPPO_LW(2, true, 1);
+      else DPPO_LW(2, false, 1);
+    }
+  } else {
+    if (n2) {
+      if (c) DPPO_LW(4, true, 2);
+      else DPPO_LW(4, false, 2);
+    } else {
+      if (c) DPPO_LW(4, true, 1);
+      else DPPO_LW(4, false, 1);
+    }
+  }
+#undef DPPO_LW
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+}  // namespace dppo

@@ -48,7 +48,9 @@ def main():
     idx = torch.randperm(T * Nn, device=dev)[:mb].to(torch.int32)
     g = torch.zeros(L.flat.total, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    for _ in range(3):
+    # WARM_LAUNCHES: back-to-back launches before the traced one, so that the in-kernel clock
+    # below is the one the chip holds under sustained load (MI355X_MICROARCH.md, DVFS give-back)
+    for _ in range(int(os.environ.get("WARM_LAUNCHES", "3"))):
         N.check(h.lib.dppo_minibatch_grad_f32(h.h, L.flat.flat.data_ptr(), idx.data_ptr(), mb, mb,
                                               ctypes.byref(hp), g.data_ptr(), None, s))
     torch.cuda.synchronize()
@@ -96,6 +98,9 @@ def main():
               f"(max {epi.max()}); start skew {(rt0.max() - rt0.min()) / 100:.2f} us, end skew "
               f"{(rt1.max() - rt1.min()) / 100:.2f} us, first start -> last end "
               f"{(rt1.max() - rt0.min()) / 100:.2f} us (s_memrealtime)")
+        ghz = (ed[:, 3] - ed[:, 0]) / np.maximum(rt1 - rt0, 1) / 10.0
+        print(f"in-kernel clock: median {np.median(ghz):.3f} GHz (min {ghz.min():.3f}, "
+              f"max {ghz.max():.3f}) over workgroups")
     if hasattr(h.lib, "dppo_debug_heads_trace"):
         hb = np.zeros((128, 4), np.int64)
         f2 = h.lib.dppo_debug_heads_trace
