@@ -13,12 +13,14 @@
 //   in lane (q, r) = feature 16b + 4q + v of sample r.  It is what the forward produces (A =
 //   weight rows, B = input) and, read as B with k-step (b, v) <-> features {16b + 4q + v}, what
 //   the next layer consumes: the forward chains in registers.
-// * T layout: register v of tile b in lane (q, r) = feature 16b + r of sample 4q + v.  The
-//   backward produces it (A = dZ in N layout, i.e. i = sample, B = W) and the weight gradient
-//   dW += dZ X^T takes both operands in it (k = sample, k-step v <-> samples {4q + v}).
+// * P layout: register v of tile b in lane (q, r) = feature 4r + b of sample 4q + v.  The
+//   backward produces it (A = dZ in N layout, i.e. i = sample; B = one ds_read_b128 of the row
+//   W[out][4r .. 4r + 3], whose four floats feed the four output tiles b) and the weight gradient
+//   dW += dZ X^T takes both operands in it (k = sample, k-step v <-> samples {4q + v}); the
+//   accumulated dW tiles come out feature-permuted and are put back in order by the epilogue.
 // Each layer therefore needs its input activation and its output delta in both layouts; the
-// N -> T / T -> N turns go through a wave-private LDS scratch (b128 one way, b32 the other,
-// conflict-free strides 68 / 72).
+// N <-> P turns go through a wave-private LDS scratch of sample-major rows (stride 68), 16-B
+// reads and writes both ways.
 //
 // ---- LDS ------------------------------------------------------------------------------------------
 // The hidden weights W2, Wa, Wc stay in LDS for the launch (read-only), rows padded to 68 floats:
@@ -41,9 +43,8 @@ namespace {
 constexpr int H = 64;
 constexpr int kWavesW = 4;                  // one wave per SIMD
 constexpr int kThreadsW = kWavesW * kWave;  // 256
-constexpr int kSmN = 68;                    // N -> T scratch: [16 samples][68]
-constexpr int kSmT = 72;                    // T -> N scratch: [16 samples][72]
-constexpr int kSlot = 16 * kSmT;                      // one turn slot (either stride)
+constexpr int kSm = 68;                     // turn scratch: [16 samples][68]
+constexpr int kSlot = 16 * kSm;                       // one turn slot
 constexpr int kScratch = 4 * kSlot + 16 * 8;          // floats per wave: 4 slots + head deltas
 constexpr int kMat = H * H;                 // one hidden weight matrix
 constexpr float kLogSqrt2PiW = 0.91893853320467274178f;
@@ -63,7 +64,18 @@ __device__ long long g_mbw_edges[256][6];
   do {                                                                  \
     if (threadIdx.x == 0 && blockIdx.x < 256) g_mbw_edges[blockIdx.x][i] = (v); \
   } while (0)
+// workgroup 0: s_memtime of every wave at each phase fence of its first 16 groups
+constexpr int kTrGroups = 16, kTrPhases = 10;
+__device__ long long g_mbw_phase[kWavesW][kTrGroups][kTrPhases];
+#define WSTAMP(k, i)                                                                     \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (k) < kTrGroups)                   \
+      g_mbw_phase[threadIdx.x >> 6][(k)][(i)] = __builtin_amdgcn_s_memtime();            \
+  } while (0)
 #else
+#define WSTAMP(k, i) \
+  do {               \
+  } while (0)
 #define WEDGE(i, v) \
   do {              \
   } while (0)
@@ -136,21 +148,41 @@ constexpr WLds make_wlds(int D16) {
 constexpr int kSmallW = 4 * H + 5 * H + 16;  // biases | Wo rows (<= 4) | Wv | scalars
 constexpr int kEpiFloats = 2 * kWavesW * kMat + kWavesW * kSmallW;
 
+// Instruction-group pins for the scheduler (llvm.amdgcn.sched.group.barrier): under the register
+// pressure of one wave per SIMD it otherwise re-uses one operand buffer and waits on every LDS read
+// right before its MFMAs.  Masks: MFMA 0x8, DS read 0x100.
+#define SG_MFMA(n) __builtin_amdgcn_sched_group_barrier(0x008, (n), 0)
+#define SG_DSR(n) __builtin_amdgcn_sched_group_barrier(0x100, (n), 0)
+#define SG_VALU(n) __builtin_amdgcn_sched_group_barrier(0x002, (n), 0)
+#define SG_DSW(n) __builtin_amdgcn_sched_group_barrier(0x200, (n), 0)
+#define SG_FENCE() __builtin_amdgcn_sched_barrier(0)
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ float tanh_w(float x) {
-  // t = e^{-2|x|}, tanh = sign(x) (1 - t) / (1 + t): one exp, one hardware reciprocal
-  const float t = __expf(-2.0f * fabsf(x));
-  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
+  // tanh = 1 - 2 / (e^{2x} + 1): five instructions (v_exp, v_rcp and three plain ones) beside a
+  // wave's MFMAs; saturates to +-1 through e^{2x} = inf / 0, absolute error <= ~1.2e-7 (the
+  // cancellation near 0 costs relative, not absolute, accuracy, as in every exp-based form)
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // 2 log2(e)
+  return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
 
+// Sixteen activations stage by stage (all multiplies, all exps, ...): consecutive instructions are
+// independent, so that pinned between MFMAs each issue slot holds work that is ready.
 __device__ __forceinline__ void tanh4(f32x4 (&y)[4]) {
+  float e[16];
 #pragma unroll
-  for (int b = 0; b < 4; ++b)
+  for (int i = 0; i < 16; ++i) e[i] = y[i >> 2][i & 3] * 2.8853900817779268f;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) y[b][v] = tanh_w(y[b][v]);
+  for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) y[i >> 2][i & 3] = __builtin_fmaf(-2.0f, e[i], 1.0f);
 }
 
 // Sum over the four lanes of a sample (q = 0..3, same r): rows 0+1 and 2+3 with
@@ -171,8 +203,8 @@ __device__ __forceinline__ float dot4(f32x4 w, f32x4 x) {
 
 // Forward of one hidden layer, N -> N: y[ob] += W[16ob + i][:] x for the four 16-row output
 // blocks; the A operand of k-steps (kb, 0..3) is one ds_read_b128 of the row.
-__device__ __forceinline__ void fwd64(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4], int q,
-                                      int r) {
+__device__ __forceinline__ void fwd64_raw(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4],
+                                          int q, int r) {
   f32x4 w[2][4];
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) w[0][ob] = *(const f32x4*)(W + (16 * ob + r) * kWS + 4 * q);
@@ -189,10 +221,26 @@ __device__ __forceinline__ void fwd64(f32x4 (&y)[4], const float* W, const f32x4
       for (int ob = 0; ob < 4; ++ob) y[ob] = mfma4(w[kb & 1][ob][v], x[kb][v], y[ob]);
   }
 }
+__device__ __forceinline__ void fwd64(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4], int q,
+                                      int r) {
+  SG_FENCE();
+  fwd64_raw(y, W, x, q, r);
+  // the next k-block's four row reads go out among this block's 16 MFMAs
+  SG_DSR(4);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (kb < 3) SG_DSR(1);
+      SG_MFMA(4);
+    }
+  SG_FENCE();
+}
 
 // Two layers on the same input (actor / critic hidden): eight independent accumulation chains.
 __device__ __forceinline__ void fwd64x2(f32x4 (&y)[4], const float* W, f32x4 (&z)[4],
                                         const float* U, const f32x4 (&x)[4], int q, int r) {
+  SG_FENCE();
   f32x4 w[2][4], u[2][4];
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
@@ -218,28 +266,46 @@ __device__ __forceinline__ void fwd64x2(f32x4 (&y)[4], const float* W, f32x4 (&z
         z[ob] = mfma4(u[kb & 1][ob][v], x[kb][v], z[ob]);
       }
   }
+  SG_DSR(8);
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (kb < 3) SG_DSR(1);
+      SG_MFMA(4);
+    }
+  SG_FENCE();
 }
 
-// Backward through one hidden layer into the T layout: t[rb] += sum_out dz[out][s] W[out][16rb+c]
-// (A = dz in N layout, B = a column piece of W: ds_read_b32).
-__device__ __forceinline__ void bwdT(f32x4 (&t)[4], const float* W, const f32x4 (&dz)[4], int q,
+// Backward through one hidden layer into the P layout: t[b] += sum_out dz[out][s] W[out][4r + b]
+// (A = dz in N layout; B = W[out][4r .. 4r + 3], one ds_read_b128 per k-step for all four tiles).
+__device__ __forceinline__ void bwdP(f32x4 (&t)[4], const float* W, const f32x4 (&dz)[4], int q,
                                      int r) {
-  float b[2][4];
-  auto ld = [&](int k, int slot) {
-    const int R = 16 * (k >> 2) + 4 * q + (k & 3);
-#pragma unroll
-    for (int rb = 0; rb < 4; ++rb) b[slot][rb] = W[R * kWS + 16 * rb + r];
+  SG_FENCE();
+  f32x4 b[3];
+  auto ld = [&](int k) {
+    return *(const f32x4*)(W + (16 * (k >> 2) + 4 * q + (k & 3)) * kWS + 4 * r);
   };
-  ld(0, 0);
+  b[0] = ld(0);
+  b[1] = ld(1);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    if (k + 1 < 16) ld(k + 1, (k + 1) & 1);
+    if (k + 2 < 16) b[(k + 2) % 3] = ld(k + 2);
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) t[rb] = mfma4(dz[k >> 2][k & 3], b[k & 1][rb], t[rb]);
+    for (int rb = 0; rb < 4; ++rb) t[rb] = mfma4(dz[k >> 2][k & 3], b[k % 3][rb], t[rb]);
   }
+  // reads two k-steps ahead of their MFMAs
+  SG_DSR(2);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k + 2 < 16) SG_DSR(1);
+    SG_MFMA(4);
+  }
+  SG_FENCE();
 }
 
-// dW[16ob.., 16ib..] += dZ X^T over the group's 16 samples (both operands in T layout).
+// dW tiles += dZ X^T over the group's 16 samples (both operands in P layout, or X in the natural
+// T layout of the input features for dW1).
 template <int NIB>
 __device__ __forceinline__ void wgrad(f32x4* acc, const f32x4 (&dzt)[4], const f32x4* xt) {
 #pragma unroll
@@ -251,27 +317,29 @@ __device__ __forceinline__ void wgrad(f32x4* acc, const f32x4 (&dzt)[4], const f
         acc[ob * NIB + ib] = mfma4(dzt[ob][v], xt[ib][v], acc[ob * NIB + ib]);
 }
 
-// N -> T through the wave's scratch (sample-major rows of 68 floats).
+// N -> P through the wave's scratch (sample-major rows of kSm floats): 16-B writes of the N tiles,
+// 16-B reads of four P-layout registers (the four tiles of one sample 4q + v) each.
 __device__ __forceinline__ void put_n(float* sm, const f32x4 (&n)[4], int q, int r) {
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) *(f32x4*)(sm + r * kSmN + 16 * ob + 4 * q) = n[ob];
+  for (int ob = 0; ob < 4; ++ob) *(f32x4*)(sm + r * kSm + 16 * ob + 4 * q) = n[ob];
 }
-__device__ __forceinline__ void get_t(f32x4 (&t)[4], const float* sm, int q, int r) {
+__device__ __forceinline__ void get_p(f32x4 (&t)[4], const float* sm, int q, int r) {
 #pragma unroll
-  for (int b = 0; b < 4; ++b)
+  for (int v = 0; v < 4; ++v) {
+    const f32x4 x = *(const f32x4*)(sm + (4 * q + v) * kSm + 4 * r);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) t[b][v] = sm[(4 * q + v) * kSmN + 16 * b + r];
+    for (int b = 0; b < 4; ++b) t[b][v] = x[b];
+  }
 }
-// T -> N (rows of 72 floats).
-__device__ __forceinline__ void put_t(float* sm, const f32x4 (&t)[4], int q, int r) {
+// P -> N.
+__device__ __forceinline__ void put_p(float* sm, const f32x4 (&t)[4], int q, int r) {
 #pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) sm[(4 * q + v) * kSmT + 16 * b + r] = t[b][v];
+  for (int v = 0; v < 4; ++v)
+    *(f32x4*)(sm + (4 * q + v) * kSm + 4 * r) = (f32x4){t[0][v], t[1][v], t[2][v], t[3][v]};
 }
 __device__ __forceinline__ void get_n(f32x4 (&n)[4], const float* sm, int q, int r) {
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) n[ob] = *(const f32x4*)(sm + r * kSmT + 16 * ob + 4 * q);
+  for (int ob = 0; ob < 4; ++ob) n[ob] = *(const f32x4*)(sm + r * kSm + 16 * ob + 4 * q);
 }
 
 __device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
@@ -318,18 +386,19 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   const int nk = first < ngroups ? (ngroups - first + stride - 1) / stride : 0;
   const int R = a.R, D = a.D;
 
-  // Loads never branch: out-of-range positions read a valid address and are zeroed after.
+  // Loads never branch and loaded values are never selected on (which would wait for them):
+  // out-of-range positions read a valid address instead -- a sample past m reads sample m - 1
+  // (its deltas are zeroed through `valid`), an input column past D reads column D - 1 (it meets a
+  // zero W1 column in the forward and lands in a dW1 column the epilogue drops).
   auto fetch = [&](int k) {
     Fetch f;
     const int g0 = (first + k * stride) * 16;
     const int sn = g0 + r;
     f.sn = idxp[sn < mm ? sn : mm - 1];
-    if (sn >= mm) f.sn = 0;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int st = g0 + 4 * q + v;
       f.st[v] = idxp[st < mm ? st : mm - 1];
-      if (st >= mm) f.st[v] = 0;
     }
     return f;
   };
@@ -339,16 +408,14 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
     for (int t = 0; t < 4 * NIB; ++t) {
       const int c = 4 * t + q;
-      const float x = rn[c < D ? c : D - 1];
-      g.xn[t] = c < D ? x : 0.0f;
+      g.xn[t] = rn[c < D ? c : D - 1];
     }
 #pragma unroll
     for (int ib = 0; ib < NIB; ++ib)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int c = 16 * ib + r;
-        const float x = a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
-        g.xt[ib][v] = c < D ? x : 0.0f;
+        g.xt[ib][v] = a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
       }
     g.sc = *(const f32x4*)(rn + a.D8);
     g.ca = CONT ? *(const f32x4*)(rn + a.D8 + 4) : z4();
@@ -360,21 +427,43 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   if (nk > 0) f_cur = fetch(0);
   if (nk > 1) f_nxt = fetch(1);
 
-  // ---------------- prologue: weights into LDS
-  for (int k = tid; k < 3 * (kMat / 4); k += kThreadsW) {
+  // ---------------- prologue: weights into LDS -- every load is issued before the first store (a
+  // load-store loop waits one memory round trip per iteration)
+  constexpr int kWLd = 3 * (kMat / 4) / kThreadsW;           // 12 f32x4 of W2 | Wa | Wc per thread
+  constexpr int kW1Ld = (H * L.RS1 + kThreadsW - 1) / kThreadsW;
+  static_assert(3 * (kMat / 4) % kThreadsW == 0 && 4 * H == kThreadsW, "prologue split");
+  f32x4 wld[kWLd];
+  float w1ld[kW1Ld];
+#pragma unroll
+  for (int i = 0; i < kWLd; ++i) {
+    const int k = tid + i * kThreadsW;
     const int mi = k >> 10, e = k & 1023, row = e >> 4, g = e & 15;
     const int64_t off = mi == 0 ? po.W2 : (mi == 1 ? po.Wa : po.Wc);
-    const f32x4 v = *(const f32x4*)(P + off + row * H + 4 * g);
-    *(f32x4*)(lds + L.W2 + mi * H * kWS + row * kWS + 4 * g) = v;
+    wld[i] = *(const f32x4*)(P + off + row * H + 4 * g);
   }
-  for (int k = tid; k < H * L.RS1; k += kThreadsW) {
+#pragma unroll
+  for (int i = 0; i < kW1Ld; ++i) {
+    const int k = tid + i * kThreadsW;
     const int row = k / L.RS1, c = k - row * L.RS1;
-    lds[L.W1 + k] = c < D ? P[po.W1 + row * D + c] : 0.0f;
+    const bool on = k < H * L.RS1 && c < D;
+    w1ld[i] = P[po.W1 + (on ? row * D + c : 0)];
   }
-  for (int k = tid; k < 4 * H; k += kThreadsW) {
-    const int h = k >> 6;
-    lds[L.Wo + k] = h < a.A ? P[po.Wo + k] : 0.0f;
+  const float wold = P[po.Wo + ((tid >> 6) < a.A ? tid : 0)];
+  GRec<NIB> g_cur{};
+  if (nk > 0) g_cur = gather(f_cur);
+#pragma unroll
+  for (int i = 0; i < kWLd; ++i) {
+    const int k = tid + i * kThreadsW;
+    const int mi = k >> 10, e = k & 1023, row = e >> 4, g = e & 15;
+    *(f32x4*)(lds + L.W2 + mi * H * kWS + row * kWS + 4 * g) = wld[i];
   }
+#pragma unroll
+  for (int i = 0; i < kW1Ld; ++i) {
+    const int k = tid + i * kThreadsW;
+    const int row = k / L.RS1, c = k - row * L.RS1;
+    if (k < H * L.RS1) lds[L.W1 + k] = c < D ? w1ld[i] : 0.0f;
+  }
+  lds[L.Wo + tid] = (tid >> 6) < a.A ? wold : 0.0f;
   if (tid < H) {
     lds[L.Wv + tid] = P[po.Wv + tid];
     lds[L.b1 + tid] = P[po.b1 + tid];
@@ -407,18 +496,16 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       }
     }
   }
-  GRec<NIB> g_cur{};
-  if (nk > 0) g_cur = gather(f_cur);
   __syncthreads();
 
   const float* W2 = lds + L.W2;
   const float* Wa = W2 + H * kWS;
   const float* Wc = W2 + 2 * H * kWS;
   // the wave's scratch: four [16 x 72] turn slots and the per-sample head-delta image [16][8]
-  float* sh1 = lds + L.scratch + wave * kScratch;  // h1 (N -> T), read back for dW2 / dz1
-  float* sh2 = sh1 + kSlot;                         // h2 (N -> T), read back for dWa, dWc / dz2
-  float* sx = sh2 + kSlot;                          // a1 (N -> T), then dza, then dz2 (T -> N)
-  float* sy = sx + kSlot;                           // c1 (N -> T), then dzc
+  float* sh1 = lds + L.scratch + wave * kScratch;  // h1 (N -> P), read back for dW2 / dz1
+  float* sh2 = sh1 + kSlot;                         // h2 (N -> P), read back for dWa, dWc / dz2
+  float* sx = sh2 + kSlot;                          // a1 (N -> P), then dza, then dz2 (P -> N)
+  float* sy = sx + kSlot;                           // c1 (N -> P), then dzc
   float* sd = sy + kSlot;                           // {dlogit[0..3], dvalue} per sample
 
   f32x4 gW2[16], gWa[16], gWc[16], gW1[4 * NIB];
@@ -426,7 +513,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   for (int i = 0; i < 16; ++i) gW2[i] = gWa[i] = gWc[i] = z4();
 #pragma unroll
   for (int i = 0; i < 4 * NIB; ++i) gW1[i] = z4();
-  // T-form partials (component b = feature 16b + r, summed over this lane's samples 4q + v)
+  // P-form partials (component b = feature 4r + b, summed over this lane's samples 4q + v)
   f32x4 gb1 = z4(), gb2 = z4(), gba = z4(), gbc = z4(), gWv = z4();
   f32x4 gWo[AMAX];
 #pragma unroll
@@ -441,6 +528,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   for (int k = 0; k < nk; ++k) {
     const int g0 = (first + k * stride) * 16;
     const bool valid = g0 + r < mm;
+    WSTAMP(k, 0);
     // ---- (1) layer 1: h1 = tanh(W1 x + b1); k-step t covers inputs {4t + q}
     f32x4 h1[4];
 #pragma unroll
@@ -456,6 +544,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     tanh4(h1);
     put_n(sh1, h1, q, r);
     PHASE_FENCE();
+    WSTAMP(k, 1);
     // ---- (2) layer 2
     f32x4 h2[4];
 #pragma unroll
@@ -464,29 +553,54 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     tanh4(h2);
     put_n(sh2, h2, q, r);
     PHASE_FENCE();
+    WSTAMP(k, 2);
     // ---- (3) actor / critic hidden layers
+    // the actor layer first; the critic layer's MFMAs then run beside the actor's tanh, its
+    // scratch turn and the actor head (VALU)
     f32x4 a1[4], c1[4];
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) {
-      a1[ob] = *(const f32x4*)(lds + L.ba + 16 * ob + 4 * q);
-      c1[ob] = *(const f32x4*)(lds + L.bc + 16 * ob + 4 * q);
+    for (int ob = 0; ob < 4; ++ob) a1[ob] = *(const f32x4*)(lds + L.ba + 16 * ob + 4 * q);
+    fwd64(a1, Wa, h2, q, r);
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) c1[ob] = *(const f32x4*)(lds + L.bc + 16 * ob + 4 * q);
+    float out[AMAX];
+    SG_FENCE();
+    {
+      f32x4 wo[AMAX][4];
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h)
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+          wo[h][ob] = *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q);
+      fwd64_raw(c1, Wc, h2, q, r);
+      tanh4(a1);
+      put_n(sx, a1, q, r);
+      // ---- (4) heads: logits / means and value of sample r, in every lane of the sample
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h) {
+        float s = 0.f;
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) s += dot4(wo[h][ob], a1[ob]);
+        out[h] = qsum(s) + lds[L.bo + h];
+      }
+      SG_DSR(4 + 4 * AMAX);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (kb < 3) SG_DSR(1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            SG_MFMA(1);
+            SG_VALU(2);
+          }
+        }
+      SG_FENCE();
     }
-    fwd64x2(a1, Wa, c1, Wc, h2, q, r);
-    tanh4(a1);
     tanh4(c1);
-    put_n(sx, a1, q, r);
     put_n(sy, c1, q, r);
     PHASE_FENCE();
-    // ---- (4) heads: logits / means and value of sample r, in every lane of the sample
-    float out[AMAX];
-#pragma unroll
-    for (int h = 0; h < AMAX; ++h) {
-      float s = 0.f;
-#pragma unroll
-      for (int ob = 0; ob < 4; ++ob)
-        s += dot4(*(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q), a1[ob]);
-      out[h] = qsum(s) + lds[L.bo + h];
-    }
+    WSTAMP(k, 3);
     float vpart = 0.f;
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
@@ -561,12 +675,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       sd[8 * r + 4] = dv;
     }
     PHASE_FENCE();
-    // ---- (6) head weight gradients (T layout: feature 16cb + r, samples 4q + v), then the head
+    WSTAMP(k, 4);
+    // ---- (6) head weight gradients (P layout: feature 4r + cb, samples 4q + v), then the head
     // back-propagation dza = (Wo^T dl)(1 - a1^2), dzc = Wv dv (1 - c1^2) in the N layout
     {
       f32x4 a1t[4], c1t[4];
-      get_t(a1t, sx, q, r);
-      get_t(c1t, sy, q, r);
+      get_p(a1t, sx, q, r);
+      get_p(c1t, sy, q, r);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const f32x4 d4 = *(const f32x4*)(sd + 8 * (4 * q + v));
@@ -592,21 +707,23 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     put_n(sx, dza, q, r);
     put_n(sy, dzc, q, r);
     PHASE_FENCE();
-    // ---- (7) dh2 = Wa^T dza + Wc^T dzc (T layout)
+    WSTAMP(k, 5);
+    // ---- (7) dh2 = Wa^T dza + Wc^T dzc (P layout)
     f32x4 dh2[4] = {z4(), z4(), z4(), z4()};
-    bwdT(dh2, Wa, dza, q, r);
-    bwdT(dh2, Wc, dzc, q, r);
+    bwdP(dh2, Wa, dza, q, r);
+    bwdP(dh2, Wc, dzc, q, r);
     // the next group's records (its indices came one group ago) and the indices after that
     GRec<NIB> g_nxt{};
     if (k + 1 < nk) g_nxt = gather(f_nxt);
     if (k + 2 < nk) f_nxt = fetch(k + 2);
     PHASE_FENCE();
+    WSTAMP(k, 6);
     // ---- (8) dz2 = dh2 (1 - h2^2); hidden-bias partials; dWa, dWc
     {
       f32x4 h2t[4], dzat[4], dzct[4], dz2t[4];
-      get_t(dzat, sx, q, r);
-      get_t(dzct, sy, q, r);
-      get_t(h2t, sh2, q, r);
+      get_p(dzat, sx, q, r);
+      get_p(dzct, sy, q, r);
+      get_p(h2t, sh2, q, r);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         dz2t[b] = dh2[b] * (1.0f - h2t[b] * h2t[b]);
@@ -614,23 +731,21 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         gbc[b] += (dzct[b][0] + dzct[b][1]) + (dzct[b][2] + dzct[b][3]);
         gb2[b] += (dz2t[b][0] + dz2t[b][1]) + (dz2t[b][2] + dz2t[b][3]);
       }
-      put_t(sx, dz2t, q, r);
+      put_p(sx, dz2t, q, r);
       wgrad<4>(gWa, dzat, h2t);
       wgrad<4>(gWc, dzct, h2t);
     }
     PHASE_FENCE();
+    WSTAMP(k, 7);
     // ---- (9) dh1 = W2^T dz2 ; dz1 = dh1 (1 - h1^2) ; dW2 ; dW1
     {
       f32x4 dz2[4], dz2t[4], h1t[4];
       get_n(dz2, sx, q, r);
       f32x4 dh1[4] = {z4(), z4(), z4(), z4()};
-      bwdT(dh1, W2, dz2, q, r);
-      // dz2 again in the T layout (from the same slot) and h1 for dW2
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) dz2t[b][v] = sx[(4 * q + v) * kSmT + 16 * b + r];
-      get_t(h1t, sh1, q, r);
+      bwdP(dh1, W2, dz2, q, r);
+      // dz2 again in the P layout (from the same slot) and h1 for dW2
+      get_p(dz2t, sx, q, r);
+      get_p(h1t, sh1, q, r);
       wgrad<4>(gW2, dz2t, h1t);
       f32x4 dz1t[4];
 #pragma unroll
@@ -642,6 +757,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
     g_cur = g_nxt;
     PHASE_FENCE();
+    WSTAMP(k, 8);
   }
 #ifdef DPPO_PHASE_TRACE
   WEDGE(2, (long long)__builtin_amdgcn_s_memtime());
@@ -652,15 +768,27 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   float* stg0 = lds;
   float* stg1 = lds + kWavesW * kMat;
   float* small = lds + 2 * kWavesW * kMat;
-  auto put_mat = [&](float* stg, const f32x4* acc, int nib, int cols) {
+  // dW tile (ob, ib) of lane (q, r), register v = dW[out 16q + 4v + ob][in]: in = 4r + ib for the
+  // hidden matrices (both operands in P layout), 16ib + r for W1 (input features in order)
+  auto put_hid = [&](float* stg, const f32x4* acc) {
     float* s = stg + wave * kMat;
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
-      for (int ib = 0; ib < nib; ++ib) {
-        const int col = 16 * ib + r;
-        if (col < cols) {
 #pragma unroll
-          for (int v = 0; v < 4; ++v) s[(16 * ob + 4 * q + v) * cols + col] = acc[ob * nib + ib][v];
+      for (int v = 0; v < 4; ++v)
+        *(f32x4*)(s + (16 * q + 4 * v + ob) * H + 4 * r) =
+            (f32x4){acc[ob * 4 + 0][v], acc[ob * 4 + 1][v], acc[ob * 4 + 2][v], acc[ob * 4 + 3][v]};
+  };
+  auto put_w1 = [&](float* stg, const f32x4* acc) {
+    float* s = stg + wave * kMat;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int ib = 0; ib < NIB; ++ib) {
+        const int col = 16 * ib + r;
+        if (col < D) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) s[(16 * q + 4 * v + ob) * D + col] = acc[ob * NIB + ib][v];
         }
       }
   };
@@ -673,10 +801,10 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
   };
   __syncthreads();  // every wave is done with the weights and its scratch
-  put_mat(stg0, gW2, 4, H);
-  put_mat(stg1, gWa, 4, H);
+  put_hid(stg0, gW2);
+  put_hid(stg1, gWa);
   {
-    // small items of this wave: hidden biases and head weights (T form: reduce over q), head
+    // small items of this wave: hidden biases and head weights (P form: reduce over q), head
     // biases / log-std / loss sums (every lane)
     float* s = small + wave * kSmallW;
 #pragma unroll
@@ -687,7 +815,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int h = 0; h < AMAX; ++h) xo[h] = qsum(gWo[h][b]);
       if (q == 0) {
-        const int f = 16 * b + r;
+        const int f = 4 * r + b;
         s[0 * H + f] = x1;
         s[1 * H + f] = x2;
         s[2 * H + f] = xa;
@@ -745,8 +873,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
   }
   __syncthreads();  // stg0 / stg1 reused
-  put_mat(stg0, gWc, 4, H);
-  put_mat(stg1, gW1, NIB, D);
+  put_hid(stg0, gWc);
+  put_w1(stg1, gW1);
   __syncthreads();
   sum_mat(stg0, po.Wc, kMat / 4);
   sum_mat(stg1, po.W1, H * D / 4);
@@ -763,6 +891,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #ifdef DPPO_PHASE_TRACE
 extern "C" __attribute__((visibility("default"))) int dppo_debug_mbw_edges(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbw_edges), sizeof(g_mbw_edges)) == hipSuccess
+             ? 0
+             : -2;
+}
+extern "C" __attribute__((visibility("default"))) int dppo_debug_mbw_phase(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbw_phase), sizeof(g_mbw_phase)) == hipSuccess
              ? 0
              : -2;
 }

@@ -49,3 +49,67 @@ extern "C" int probe_mfma(int nacc, float* out, long long* cyc, int iters, int w
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Does VALU work co-issue with fp32 MFMAs on one SIMD?  Each active wave runs 4 MFMA accumulator
+// chains and NV independent v_fma_f32 chains per MFMA (mode 0); mode 1 splits the two across the
+// two waves of each SIMD (waves 0-3: MFMAs only, waves 4-7: the same VALU work only).
+template <int NV>
+__global__ __launch_bounds__(512) void mfma_valu(float* out, long long* cyc, int iters, int mode) {
+  const int wave = threadIdx.x >> 6;
+  f32x4 acc[4];
+  float x[8];
+  for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, (float)threadIdx.x};
+  for (int i = 0; i < 8; ++i) x[i] = threadIdx.x * 1e-3f + i;
+  float a = 1.0f + threadIdx.x * 1e-3f, b = 0.5f, c = 0.999f, d = 1e-3f;
+  const int w = __builtin_amdgcn_readfirstlane(wave);
+  const int role = mode == 0 ? 0 : (w < 4 ? 1 : 2);  // 0: both, 1: MFMA only, 2: VALU only
+  long long t0 = __builtin_amdgcn_s_memtime();
+  if (role == 0) {
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+#pragma unroll
+          for (int v = 0; v < NV; ++v) x[v] = __builtin_fmaf(x[v], c, d);
+        }
+    }
+  } else if (role == 1) {
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+    }
+  } else {
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) x[v] = __builtin_fmaf(x[v], c, d);
+    }
+  }
+  float s = 0.f;
+  for (int i = 0; i < 4; ++i) s += acc[i][0] + acc[i][3];
+  for (int i = 0; i < 8; ++i) s += x[i];
+  long long t1 = __builtin_amdgcn_s_memtime();
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 8 + wave] = t1 - t0;
+}
+
+extern "C" int probe_mfma_valu(int nv, int mode, float* out, long long* cyc, int iters, int blocks,
+                               void* stream) {
+  dim3 g(blocks), b(mode == 0 ? 256 : 512);
+  hipStream_t s = (hipStream_t)stream;
+  switch (nv) {
+    case 0: hipLaunchKernelGGL(mfma_valu<0>, g, b, 0, s, out, cyc, iters, mode); break;
+    case 1: hipLaunchKernelGGL(mfma_valu<1>, g, b, 0, s, out, cyc, iters, mode); break;
+    case 2: hipLaunchKernelGGL(mfma_valu<2>, g, b, 0, s, out, cyc, iters, mode); break;
+    case 4: hipLaunchKernelGGL(mfma_valu<4>, g, b, 0, s, out, cyc, iters, mode); break;
+    case 6: hipLaunchKernelGGL(mfma_valu<6>, g, b, 0, s, out, cyc, iters, mode); break;
+    case 8: hipLaunchKernelGGL(mfma_valu<8>, g, b, 0, s, out, cyc, iters, mode); break;
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
