@@ -67,6 +67,12 @@ __device__ long long g_mbw_edges[256][6];
 // workgroup 0: s_memtime of every wave at each phase fence of its first 16 groups
 constexpr int kTrGroups = 16, kTrPhases = 10;
 __device__ long long g_mbw_phase[kWavesW][kTrGroups][kTrPhases];
+// workgroup 0, thread 0: s_memtime at the steps of the epilogue
+__device__ long long g_mbw_epi[8];
+#define ESTAMP(i)                                                                        \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_mbw_epi[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #define WSTAMP(k, i)                                                                     \
   do {                                                                                   \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (k) < kTrGroups)                   \
@@ -75,6 +81,9 @@ __device__ long long g_mbw_phase[kWavesW][kTrGroups][kTrPhases];
 #else
 #define WSTAMP(k, i) \
   do {               \
+  } while (0)
+#define ESTAMP(i) \
+  do {            \
   } while (0)
 #define WEDGE(i, v) \
   do {              \
@@ -195,6 +204,20 @@ __device__ __forceinline__ float qsum(float x) {
   const auto p2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false,
                                                    false);
   return __uint_as_float(p2[0]) + __uint_as_float(p2[1]);
+}
+
+// Sum over each 16-lane row (the result in every lane of the row) with DPP lane moves: lane ^ 1,
+// lane ^ 2, the mirrored half-row, the mirrored row.
+template <int CTRL>
+__device__ __forceinline__ float dppw(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16(float x) {
+  x += dppw<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dppw<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dppw<0x141>(x);  // row_half_mirror
+  x += dppw<0x140>(x);  // row_mirror
+  return x;
 }
 
 __device__ __forceinline__ float dot4(f32x4 w, f32x4 x) {
@@ -800,51 +823,59 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       slab_st4(slab + off + 4 * c, v);
     }
   };
+  // register-only reductions of this wave's small items first (they overlap the wait for the
+  // slowest wave): hidden biases and head weights (P form: sum over q), head biases / log-std /
+  // loss sums (every lane: 16-lane rows by DPP, then the four rows)
+  float xs[4][5 + AMAX];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    xs[b][0] = qsum(gb1[b]);
+    xs[b][1] = qsum(gb2[b]);
+    xs[b][2] = qsum(gba[b]);
+    xs[b][3] = qsum(gbc[b]);
+    xs[b][4] = qsum(gWv[b]);
+#pragma unroll
+    for (int h = 0; h < AMAX; ++h) xs[b][5 + h] = qsum(gWo[h][b]);
+  }
+  float sc[2 * AMAX + 4];
+#pragma unroll
+  for (int h = 0; h < AMAX; ++h) {
+    sc[h] = gbo[h];
+    sc[AMAX + h] = gls[h];
+  }
+  sc[2 * AMAX] = gbv;
+  sc[2 * AMAX + 1] = s_pi;
+  sc[2 * AMAX + 2] = s_v;
+  sc[2 * AMAX + 3] = s_ent;
+#pragma unroll
+  for (int j = 0; j < 2 * AMAX + 4; ++j) sc[j] = qsum(row16(sc[j]));
   __syncthreads();  // every wave is done with the weights and its scratch
+  ESTAMP(0);
   put_hid(stg0, gW2);
   put_hid(stg1, gWa);
   {
-    // small items of this wave: hidden biases and head weights (P form: reduce over q), head
-    // biases / log-std / loss sums (every lane)
     float* s = small + wave * kSmallW;
+    if (q == 0) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const float x1 = qsum(gb1[b]), x2 = qsum(gb2[b]), xa = qsum(gba[b]), xc = qsum(gbc[b]);
-      const float xv = qsum(gWv[b]);
-      float xo[AMAX];
-#pragma unroll
-      for (int h = 0; h < AMAX; ++h) xo[h] = qsum(gWo[h][b]);
-      if (q == 0) {
+      for (int b = 0; b < 4; ++b) {
         const int f = 4 * r + b;
-        s[0 * H + f] = x1;
-        s[1 * H + f] = x2;
-        s[2 * H + f] = xa;
-        s[3 * H + f] = xc;
+        s[0 * H + f] = xs[b][0];
+        s[1 * H + f] = xs[b][1];
+        s[2 * H + f] = xs[b][2];
+        s[3 * H + f] = xs[b][3];
 #pragma unroll
-        for (int h = 0; h < AMAX; ++h) s[4 * H + h * H + f] = xo[h];
-        s[8 * H + f] = xv;
+        for (int h = 0; h < AMAX; ++h) s[4 * H + h * H + f] = xs[b][5 + h];
+        s[8 * H + f] = xs[b][4];
       }
     }
-    float sc[2 * AMAX + 4];
-#pragma unroll
-    for (int h = 0; h < AMAX; ++h) {
-      sc[h] = gbo[h];
-      sc[AMAX + h] = gls[h];
-    }
-    sc[2 * AMAX] = gbv;
-    sc[2 * AMAX + 1] = s_pi;
-    sc[2 * AMAX + 2] = s_v;
-    sc[2 * AMAX + 3] = s_ent;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1)
-#pragma unroll
-      for (int j = 0; j < 2 * AMAX + 4; ++j) sc[j] += __shfl_xor(sc[j], off);
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < 2 * AMAX + 4; ++j) s[9 * H + j] = sc[j];
     }
   }
+  ESTAMP(1);
   __syncthreads();
+  ESTAMP(2);
   sum_mat(stg0, po.W2, kMat / 4);
   sum_mat(stg1, po.Wa, kMat / 4);
   for (int j = tid; j < kSmallW; j += kThreadsW) {
@@ -872,12 +903,16 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       }
     }
   }
+  ESTAMP(3);
   __syncthreads();  // stg0 / stg1 reused
   put_hid(stg0, gWc);
   put_w1(stg1, gW1);
+  ESTAMP(4);
   __syncthreads();
+  ESTAMP(5);
   sum_mat(stg0, po.Wc, kMat / 4);
   sum_mat(stg1, po.W1, H * D / 4);
+  ESTAMP(6);
 #ifdef DPPO_PHASE_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -893,6 +928,9 @@ extern "C" __attribute__((visibility("default"))) int dppo_debug_mbw_edges(long 
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbw_edges), sizeof(g_mbw_edges)) == hipSuccess
              ? 0
              : -2;
+}
+extern "C" __attribute__((visibility("default"))) int dppo_debug_mbw_epi(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbw_epi), sizeof(g_mbw_epi)) == hipSuccess ? 0 : -2;
 }
 extern "C" __attribute__((visibility("default"))) int dppo_debug_mbw_phase(long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mbw_phase), sizeof(g_mbw_phase)) == hipSuccess

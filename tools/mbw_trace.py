@@ -83,6 +83,17 @@ def main():
           f"(max {epi.max()}); start skew {(rt0.max() - rt0.min()) / 100:.2f} us, end skew "
           f"{(rt1.max() - rt1.min()) / 100:.2f} us, first start -> last end "
           f"{(rt1.max() - rt0.min()) / 100:.2f} us")
+    if hasattr(h.lib, "dppo_debug_mbw_epi"):
+        ep = np.zeros(8, np.int64)
+        f4 = h.lib.dppo_debug_mbw_epi
+        f4.argtypes = [ctypes.c_void_p]
+        assert f4(ep.ctypes.data) == 0
+        names = ["put W2|Wa + small", "barrier", "sum W2|Wa + small", "barrier + put Wc|W1",
+                 "barrier", "sum Wc|W1", "drain + barrier"]
+        ep[7] = ed[0, 3]
+        print("epilogue of workgroup 0 (cycles): " + ", ".join(
+            f"{n} {ep[i + 1] - ep[i]}" for i, n in enumerate(names)) +
+            f"; loop exit -> epilogue {ep[0] - ed[0, 2]}")
     ghz = (ed[:, 3] - ed[:, 0]) / np.maximum(rt1 - rt0, 1) / 10.0
     print(f"in-kernel clock: median {np.median(ghz):.3f} GHz (min {ghz.min():.3f}, "
           f"max {ghz.max():.3f})")
