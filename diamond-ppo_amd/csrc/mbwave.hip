@@ -45,7 +45,8 @@ constexpr int kWavesW = 4;                  // one wave per SIMD
 constexpr int kThreadsW = kWavesW * kWave;  // 256
 constexpr int kSm = 68;                     // turn scratch: [16 samples][68]
 constexpr int kSlot = 16 * kSm;                       // one turn slot
-constexpr int kScratch = 4 * kSlot + 16 * 8;          // floats per wave: 4 slots + head deltas
+constexpr int kSdw = 12;                              // head-delta row: dlogit[8] | dvalue
+constexpr int kScratch = 4 * kSlot + 16 * kSdw;       // floats per wave: 4 slots + head deltas
 constexpr int kMat = H * H;                 // one hidden weight matrix
 constexpr float kLogSqrt2PiW = 0.91893853320467274178f;
 constexpr float kLn2W = 0.69314718055994530942f;
@@ -95,10 +96,10 @@ constexpr int kWS = 68;  // row stride of the hidden weight images
 struct WLds {   // offsets in floats (compile-time: one layout per input width)
   int W2;       // W2 | Wa | Wc: [3][64][kWS]
   int scratch;  // [4 waves][kScratch]
-  int Wo, Wv;   // [4][64] (rows >= A zero), [64]
+  int Wo, Wv;   // [8][64] (rows >= A zero), [64]
   int b1, b2, ba, bc;
-  int bo, bv, ls;  // [4] each
-  int gc;       // [4][4]: 1/(2 var), 1/var, 1/sigma, log sigma per action (continuous)
+  int bo, bv, ls;  // [8], [4], [8]
+  int gc;       // [4][8]: 1/(2 var), 1/var, 1/sigma, log sigma per action (continuous)
   int gent;     // [4]: {sum entropy terms, sum log-prob constants}
   int W1, RS1;  // W1 [64][RS1]
   int total;
@@ -125,7 +126,7 @@ constexpr WLds make_wlds(int D16) {
   L.scratch = o;
   o += kWavesW * kScratch;
   L.Wo = o;
-  o += 4 * H;
+  o += 8 * H;
   L.Wv = o;
   o += H;
   L.b1 = o;
@@ -137,13 +138,13 @@ constexpr WLds make_wlds(int D16) {
   L.bc = o;
   o += H;
   L.bo = o;
-  o += 4;
+  o += 8;
   L.bv = o;
   o += 4;
   L.ls = o;
-  o += 4;
+  o += 8;
   L.gc = o;
-  o += 16;
+  o += 32;
   L.gent = o;
   o += 4;
   L.W1 = o;
@@ -153,9 +154,12 @@ constexpr WLds make_wlds(int D16) {
   return L;
 }
 
-// Epilogue staging: two [4 waves][64 x 64] buffers, then the small per-wave items.
-constexpr int kSmallW = 4 * H + 5 * H + 16;  // biases | Wo rows (<= 4) | Wv | scalars
-constexpr int kEpiFloats = 2 * kWavesW * kMat + kWavesW * kSmallW;
+// Epilogue staging: two [4 waves][64 x 64] buffers, then the small per-wave items
+// {biases b1 b2 ba bc | AMAX head rows | Wv | 2 AMAX + 4 scalars}.
+constexpr int small_floats(int amax) { return (5 + amax) * H + 2 * amax + 4; }
+constexpr int epi_floats(int amax) {
+  return 2 * kWavesW * kMat + kWavesW * ((small_floats(amax) + 3) & ~3);
+}
 
 // Instruction-group pins for the scheduler (llvm.amdgcn.sched.group.barrier): under the register
 // pressure of one wave per SIMD it otherwise re-uses one operand buffer and waits on every LDS read
@@ -381,7 +385,7 @@ struct GRec {
   float xn[4 * NIB];  // layer-1 B operand: input 4t + q of sample r
   f32x4 xt[NIB];      // T layout of the input: feature 16ib + r of samples 4q + v
   f32x4 sc;           // {action bits, old log-prob, advantage, return} of sample r
-  f32x4 ca;           // continuous action of sample r (<= 4 dims)
+  f32x4 ca[2];        // continuous action of sample r (<= 8 dims)
 };
 
 template <int AMAX, bool CONT, int NIB>
@@ -441,7 +445,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         g.xt[ib][v] = a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
       }
     g.sc = *(const f32x4*)(rn + a.D8);
-    g.ca = CONT ? *(const f32x4*)(rn + a.D8 + 4) : z4();
+    g.ca[0] = CONT ? *(const f32x4*)(rn + a.D8 + 4) : z4();
+    g.ca[1] = (CONT && AMAX > 4) ? *(const f32x4*)(rn + a.D8 + 8) : z4();
     return g;
   };
 
@@ -472,6 +477,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     w1ld[i] = P[po.W1 + (on ? row * D + c : 0)];
   }
   const float wold = P[po.Wo + ((tid >> 6) < a.A ? tid : 0)];
+  const float wold2 = P[po.Wo + ((tid >> 6) + 4 < a.A ? tid + 4 * H : 0)];
   GRec<NIB> g_cur{};
   if (nk > 0) g_cur = gather(f_cur);
 #pragma unroll
@@ -487,29 +493,30 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     if (k < H * L.RS1) lds[L.W1 + k] = c < D ? w1ld[i] : 0.0f;
   }
   lds[L.Wo + tid] = (tid >> 6) < a.A ? wold : 0.0f;
+  lds[L.Wo + 4 * H + tid] = (tid >> 6) + 4 < a.A ? wold2 : 0.0f;
   if (tid < H) {
     lds[L.Wv + tid] = P[po.Wv + tid];
     lds[L.b1 + tid] = P[po.b1 + tid];
     lds[L.b2 + tid] = P[po.b2 + tid];
     lds[L.ba + tid] = P[po.ba + tid];
     lds[L.bc + tid] = P[po.bc + tid];
-  } else if (tid < H + 4) {
+  } else if (tid < H + 8) {
     const int h = tid - H;
     lds[L.bo + h] = h < a.A ? P[po.bo + h] : 0.0f;
     lds[L.ls + h] = (CONT && h < a.A) ? P[po.ls + h] : 0.0f;
-    lds[L.bv + h] = h == 0 ? P[po.bv] : 0.0f;
+    if (h < 4) lds[L.bv + h] = h == 0 ? P[po.bv] : 0.0f;
     if (CONT) {
       // Normal(mean, exp(log_std)) constants of action h (continuous_ppo.py:41-47; torch
       // Normal.log_prob / entropy), the same for every sample
       const bool on = h < a.A;
       const float sg = on ? __expf(P[po.ls + h]) : 1.0f;
       lds[L.gc + h] = on ? 1.0f / (2.0f * (sg * sg)) : 0.0f;
-      lds[L.gc + 4 + h] = 1.0f / (sg * sg);
-      lds[L.gc + 8 + h] = 1.0f / sg;
-      lds[L.gc + 12 + h] = on ? __logf(sg) : 0.0f;
+      lds[L.gc + 8 + h] = 1.0f / (sg * sg);
+      lds[L.gc + 16 + h] = 1.0f / sg;
+      lds[L.gc + 24 + h] = on ? __logf(sg) : 0.0f;
       if (h == 0) {
         float e = 0.0f, c = 0.0f;
-        for (int k = 0; k < a.A && k < 4; ++k) {
+        for (int k = 0; k < a.A && k < 8; ++k) {
           const float l = __logf(__expf(P[po.ls + k]));
           e += kHalfLog2PiPlusHalfW + l;  // entropy (continuous_ppo.py:45-47)
           c += l + kLogSqrt2PiW;           // log-prob constant part
@@ -589,12 +596,6 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     float out[AMAX];
     SG_FENCE();
     {
-      f32x4 wo[AMAX][4];
-#pragma unroll
-      for (int h = 0; h < AMAX; ++h)
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-          wo[h][ob] = *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q);
       fwd64_raw(c1, Wc, h2, q, r);
       tanh4(a1);
       put_n(sx, a1, q, r);
@@ -603,7 +604,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       for (int h = 0; h < AMAX; ++h) {
         float s = 0.f;
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) s += dot4(wo[h][ob], a1[ob]);
+        for (int ob = 0; ob < 4; ++ob)
+          s += dot4(*(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q), a1[ob]);
         out[h] = qsum(s) + lds[L.bo + h];
       }
       SG_DSR(4 + 4 * AMAX);
@@ -638,7 +640,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       float qq = 0.f;
 #pragma unroll
       for (int h = 0; h < AMAX; ++h) {
-        const float d = g_cur.ca[h] - out[h];
+        const float d = g_cur.ca[h >> 2][h & 3] - out[h];
         qq += (d * d) * lds[L.gc + h];  // 1 / (2 var): 0 past A
       }
       logp = -qq - lds[L.gent + 1];
@@ -672,13 +674,17 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     const float vm = valid ? a.inv_m : 0.f;
     const float dlogp = (gu * -adv + gw * -adv * inr) * vm * ratio;
     const float dv = a.vf * (val - ret) * vm;                       // ppo.py:272
-    float dl[4] = {0.f, 0.f, 0.f, 0.f};
+    constexpr int NDL = AMAX > 4 ? 8 : 4;
+    constexpr int kDv = NDL;  // the value delta follows the logit deltas in a head-delta row
+    float dl[NDL];
+#pragma unroll
+    for (int h = 0; h < NDL; ++h) dl[h] = 0.f;
 #pragma unroll
     for (int h = 0; h < AMAX; ++h) {
       if (CONT) {
-        const float dd = g_cur.ca[h] - out[h];
-        const float zz = dd * lds[L.gc + 8 + h];
-        dl[h] = h < a.A ? dlogp * dd * lds[L.gc + 4 + h] : 0.f;
+        const float dd = g_cur.ca[h >> 2][h & 3] - out[h];
+        const float zz = dd * lds[L.gc + 16 + h];
+        dl[h] = h < a.A ? dlogp * dd * lds[L.gc + 8 + h] : 0.f;
         if (q == 0 && h < a.A) gls[h] += dlogp * (zz * zz - 1.0f);
       } else {
         const int actn = __float_as_int(sc[0]);
@@ -694,8 +700,10 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int h = 0; h < AMAX; ++h) gbo[h] += dl[h];
       gbv += dv;
-      *(f32x4*)(sd + 8 * r) = (f32x4){dl[0], dl[1], dl[2], dl[3]};
-      sd[8 * r + 4] = dv;
+#pragma unroll
+      for (int c = 0; c < NDL / 4; ++c)
+        *(f32x4*)(sd + kSdw * r + 4 * c) = (f32x4){dl[4 * c], dl[4 * c + 1], dl[4 * c + 2], dl[4 * c + 3]};
+      sd[kSdw * r + kDv] = dv;
     }
     PHASE_FENCE();
     WSTAMP(k, 4);
@@ -707,12 +715,14 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       get_p(c1t, sy, q, r);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const f32x4 d4 = *(const f32x4*)(sd + 8 * (4 * q + v));
-        const float dvs = sd[8 * (4 * q + v) + 4];
+        f32x4 d4[NDL / 4];
+#pragma unroll
+        for (int c = 0; c < NDL / 4; ++c) d4[c] = *(const f32x4*)(sd + kSdw * (4 * q + v) + 4 * c);
+        const float dvs = sd[kSdw * (4 * q + v) + kDv];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
 #pragma unroll
-          for (int h = 0; h < AMAX; ++h) gWo[h][cb] += d4[h] * a1t[cb][v];
+          for (int h = 0; h < AMAX; ++h) gWo[h][cb] += d4[h >> 2][h & 3] * a1t[cb][v];
           gWv[cb] += dvs * c1t[cb][v];
         }
       }
@@ -791,6 +801,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   float* stg0 = lds;
   float* stg1 = lds + kWavesW * kMat;
   float* small = lds + 2 * kWavesW * kMat;
+  constexpr int kSmallW = (small_floats(AMAX) + 3) & ~3;
   // dW tile (ob, ib) of lane (q, r), register v = dW[out 16q + 4v + ob][in]: in = 4r + ib for the
   // hidden matrices (both operands in P layout), 16ib + r for W1 (input features in order)
   auto put_hid = [&](float* stg, const f32x4* acc) {
@@ -865,12 +876,12 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         s[3 * H + f] = xs[b][3];
 #pragma unroll
         for (int h = 0; h < AMAX; ++h) s[4 * H + h * H + f] = xs[b][5 + h];
-        s[8 * H + f] = xs[b][4];
+        s[(4 + AMAX) * H + f] = xs[b][4];
       }
     }
     if (lane == 0) {
 #pragma unroll
-      for (int j = 0; j < 2 * AMAX + 4; ++j) s[9 * H + j] = sc[j];
+      for (int j = 0; j < 2 * AMAX + 4; ++j) s[(5 + AMAX) * H + j] = sc[j];
     }
   }
   ESTAMP(1);
@@ -885,13 +896,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       const int l = j >> 6, f = j & 63;
       const int64_t off = l == 0 ? po.b1 : (l == 1 ? po.b2 : (l == 2 ? po.ba : po.bc));
       slab[off + f] = v;
-    } else if (j < 8 * H) {
+    } else if (j < (4 + AMAX) * H) {
       const int h = (j - 4 * H) >> 6, f = j & 63;
-      if (h < a.A && h < AMAX) slab[po.Wo + h * H + f] = v;
-    } else if (j < 9 * H) {
-      slab[po.Wv + (j - 8 * H)] = v;
+      if (h < a.A) slab[po.Wo + h * H + f] = v;
+    } else if (j < (5 + AMAX) * H) {
+      slab[po.Wv + (j - (4 + AMAX) * H)] = v;
     } else {
-      const int e = j - 9 * H;
+      const int e = j - (5 + AMAX) * H;
       if (e < AMAX) {
         if (e < a.A) slab[po.bo + e] = v;
       } else if (e < 2 * AMAX) {
@@ -944,7 +955,11 @@ bool mbw_supported(const MlpShape& sh) {
     const char* e = std::getenv("DPPO_MB_LEGACY");
     return e && e[0] == '1' ? 1 : 0;
   }();
-  return !legacy && sh.A <= 4 && sh.D <= 32;
+  // Up to 4 actions at any input width; 5-8 only for discrete heads on <= 16 inputs: the other
+  // 8-action instantiations spill registers and lose to the two-team kernel (HalfCheetah, D = 17,
+  // A = 6: 92 vs 77 us per launch).
+  if (legacy || sh.D > 32) return false;
+  return sh.A <= 4 || (sh.A <= 8 && !sh.continuous && sh.D <= 16);
 }
 
 int mbw_grid(int32_t m) {
@@ -957,7 +972,8 @@ int mbw_grid(int32_t m) {
 size_t mbw_lds_bytes(const MlpShape& sh) {
   const int D16 = (sh.D + 15) / 16 * 16;
   const WLds L = make_wlds(D16);
-  const int n = L.total > kEpiFloats ? L.total : kEpiFloats;
+  const int epi = epi_floats(sh.A <= 2 ? 2 : (sh.A <= 4 ? 4 : 8));
+  const int n = L.total > epi ? L.total : epi;
   return (size_t)n * sizeof(float);
 }
 
@@ -996,29 +1012,27 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     DPPO_SETW(2, false, 1) DPPO_SETW(2, true, 1) DPPO_SETW(4, false, 1) DPPO_SETW(4, true, 1)
     DPPO_SETW(2, false, 2) DPPO_SETW(2, true, 2) DPPO_SETW(4, false, 2) DPPO_SETW(4, true, 2)
+    DPPO_SETW(8, false, 1)
 #undef DPPO_SETW
   }
   const dim3 grid((unsigned)G), block(kThreadsW);
   const bool c = sh.continuous != 0;
   const bool n2 = D16 > 16;
 #define DPPO_LW(A, C, N) DPPO_LAUNCH((mbw_kernel<A, C, N>), grid, block, lds, s, k)
-  if (sh.A <= 2) {
-    if (n2) {
-      if (c) DPPO_LW(2, true, 2);
-      else DPPO_LW(2, false, 2);
-    } else {
-      if (c) DPPO_LW(2, true, 1);
-      else DPPO_LW(2, false, 1);
-    }
-  } else {
-    if (n2) {
-      if (c) DPPO_LW(4, true, 2);
-      else DPPO_LW(4, false, 2);
-    } else {
-      if (c) DPPO_LW(4, true, 1);
-      else DPPO_LW(4, false, 1);
-    }
-  }
+#define DPPO_LWC(A)                      \
+  do {                                   \
+    if (n2) {                            \
+      if (c) DPPO_LW(A, true, 2);        \
+      else DPPO_LW(A, false, 2);         \
+    } else {                             \
+      if (c) DPPO_LW(A, true, 1);        \
+      else DPPO_LW(A, false, 1);         \
+    }                                    \
+  } while (0)
+  if (sh.A <= 2) DPPO_LWC(2);
+  else if (sh.A <= 4) DPPO_LWC(4);
+  else DPPO_LW(8, false, 1);  // mbw_supported: discrete, D <= 16
+#undef DPPO_LWC
 #undef DPPO_LW
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;

@@ -73,6 +73,24 @@ def hparams():
 
 
 def nit_of(m):
+    """32-sample steps per workgroup of the two-team kernel (mbstep.hip)."""
     steps = (m + 31) // 32
     G = min(steps, 256)
     return (steps + G - 1) // G
+
+
+def sample_split(D, A, cont):
+    """Whether learn() runs the sample-split kernel (mbwave.hip, mbw_supported) for this shape."""
+    return D <= 32 and (A <= 4 or (A <= 8 and not cont and D <= 16))
+
+
+def groups_per_wave(m):
+    """16-sample groups each wave of the sample-split kernel runs (4 waves per workgroup, one
+    workgroup per 64 samples up to 256)."""
+    groups = (m + 15) // 16
+    G = min((m + 63) // 64, 256)
+    return (groups + 4 * G - 1) // (4 * G)
+
+
+def production_depth(m, D, A, cont):
+    return groups_per_wave(m) if sample_split(D, A, cont) else nit_of(m)

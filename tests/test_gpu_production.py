@@ -1,11 +1,17 @@
-"""GPU parity of the minibatch kernel in its PRODUCTION configuration.
+"""GPU parity of the minibatch kernels in their PRODUCTION configuration.
 
-``mb_kernel`` (csrc/mbstep.hip) launches G = min(ceil(m/32), 256) workgroups; each runs
-nit = ceil(ceil(m/32)/G) 32-sample steps through a two-team software pipeline (the forward team on
-step it while the backward team back-propagates step it-1, hand-off images double-buffered by step
-parity).  The golden-trace tests have minibatches of at most 4,096 samples, i.e. nit == 1: only
-one team is ever busy per interval set and the odd-parity buffers are never read.  Every BASELINE
-configuration runs nit = 8 (C2, C4) or 16 (C3).  These tests run those shapes:
+Two kernels compute a minibatch gradient (csrc/common.h launch_mb):
+* the sample-split kernel (csrc/mbwave.hip; <= 4 actions, or <= 8 discrete on <= 16 inputs):
+  G = min(ceil(m/64), 256) workgroups of 4 waves, each wave running ceil(ceil(m/16) / 4G)
+  16-sample groups end to end and accumulating its own weight gradients across them (C2: 4
+  groups per wave, C3: 8).  The golden-trace tests have minibatches of at most 4,096 samples, i.e.
+  one group per wave: the cross-group accumulation and prefetch are first exercised here;
+* the two-team kernel (csrc/mbstep.hip; HalfCheetah's 6 continuous actions on 17 inputs):
+  G = min(ceil(m/32), 256) workgroups, each running nit = ceil(ceil(m/32)/G) 32-sample steps
+  through a two-team software pipeline (the forward team on step it while the backward team
+  back-propagates step it-1, hand-off images double-buffered by step parity); small minibatches
+  have nit == 1 and never read the odd-parity buffers.  C4 runs nit = 8.
+These tests run the production shapes:
 
 * one minibatch gradient at the full C2 / C3 / C4 minibatch sizes (65,536 / 131,072 / 65,536
   samples, nit = 8 / 16 / 8), plus a ragged one (m % 32 != 0, workgroups with unequal step
@@ -36,7 +42,8 @@ import diamond
 from diamond import _native as N
 from oracle import ppo_np as P
 
-from gpu_helpers import H, SpecEnvs, dev, hparams, nit_of, random_params, stream, synth
+from gpu_helpers import (H, SpecEnvs, dev, hparams, production_depth, random_params, stream,
+                         synth)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -46,6 +53,8 @@ from gpu_helpers import H, SpecEnvs, dev, hparams, nit_of, random_params, stream
     ("C4 cheetah", 128, 4096, 17, 6, True, 0),
     ("C2 ragged", 128, 4096, 4, 2, False, 77),
     ("C4 ragged", 128, 4096, 17, 6, True, 4093),
+    ("7 discrete actions", 128, 4096, 6, 7, False, 0),
+    ("3 Gaussian actions, 20 inputs", 128, 4096, 20, 3, True, 13),
 ])
 def test_full_minibatch_gradient_vs_oracle(name, T, Nn, D, A, cont, ragged):
     E, M = 4, 8
@@ -65,7 +74,7 @@ def test_full_minibatch_gradient_vs_oracle(name, T, Nn, D, A, cont, ragged):
     N.check(h.lib.dppo_prepare_f32(h.h, ctypes.byref(ro.as_struct()), pd.data_ptr(),
                                    ctypes.byref(hp), ctypes.byref(lo), stream()))
     mb = B // M - ragged
-    assert nit_of(mb) >= 8
+    assert production_depth(mb, D, A, cont) >= 4
     idx = np.random.RandomState(B).permutation(B)[:mb].astype(np.int32)
     idx_d = torch.from_numpy(idx).to(dev())
     g = torch.zeros(L.total, device=dev())
@@ -167,21 +176,24 @@ def learn_vs_oracle(T, Nn, D, A, cont, seed):
     return mb
 
 
-@pytest.mark.parametrize("T,Nn,D,A,cont,want_nit", [
-    (128, 1024, 4, 2, False, 2),     # mb 16,384: every workgroup two steps
-    (128, 1536, 8, 4, False, 3),     # mb 24,576: three steps
-    (128, 768, 17, 6, True, 2),      # mb 12,288: 384 steps over 256 workgroups (ragged nit)
-    (100, 1000, 5, 3, False, 2),     # mb 12,500: 391 steps, the last one partial
+@pytest.mark.parametrize("T,Nn,D,A,cont,want_depth", [
+    (128, 2048, 4, 2, False, 2),     # sample-split, mb 32,768: two groups per wave
+    (128, 1536, 8, 4, False, 2),     # 1,536 groups over 1,024 waves: some waves two, some one
+    (100, 3000, 5, 3, False, 3),     # mb 37,500: three groups per wave, the last group partial
+    (100, 1000, 5, 3, False, 1),     # mb 12,500: 196 workgroups, the last group partial
+    (128, 2048, 3, 1, True, 2),      # Gaussian head on the sample-split kernel
+    (128, 768, 17, 6, True, 2),      # two-team kernel: 384 steps over 256 workgroups (ragged nit)
 ])
-def test_learn_intermediate_nit_vs_oracle(T, Nn, D, A, cont, want_nit):
+def test_learn_intermediate_depth_vs_oracle(T, Nn, D, A, cont, want_depth):
     mb = learn_vs_oracle(T, Nn, D, A, cont, seed=T + Nn)
-    assert nit_of(mb) == want_nit
+    assert production_depth(mb, D, A, cont) == want_depth
 
 
 def test_learn_full_c2_vs_oracle():
-    """BASELINE configs[1] itself: CartPole PPO, T = 128, N = 4096 (mb 65,536, nit = 8)."""
+    """BASELINE configs[1] itself: CartPole PPO, T = 128, N = 4096 (mb 65,536: four groups per
+    wave of the sample-split kernel)."""
     mb = learn_vs_oracle(128, 4096, 4, 2, False, seed=0)
-    assert nit_of(mb) == 8
+    assert production_depth(mb, 4, 2, False) == 4
 
 
 # ---------------------------------------------------------------------------------------------
