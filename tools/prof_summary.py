@@ -23,7 +23,7 @@ import re
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLASS = {"mb_kernel": "grad", "grad_kernel": "grad", "eval_kernel": "eval", "gae_kernel": "gae", "gae_pipe_kernel": "gae",
+CLASS = {"mb_kernel": "grad", "mbw_kernel": "grad", "grad_kernel": "grad", "eval_kernel": "eval", "gae_kernel": "gae", "gae_pipe_kernel": "gae",
          "pack_kernel": "pack", "slab_reduce_kernel": "slab_reduce",
          "clip_adam_kernel": "clip_adam", "reduce_adam_kernel": "reduce_adam",
          "stats_reduce_kernel": "adv_stats", "fy_build_kernel": "perm",
