@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ val,
     const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
-    double* __restrict__ partials, int T, int N, float g, float c, int wt) {
+    double* __restrict__ partials, int T, int N, float g, float c, int wt, int stagger) {
   __shared__ __attribute__((aligned(16))) PipeLds<E> L;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ntiles = N / E;
@@ -276,6 +276,13 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     const int e0 = 4 * (lane % V4);
     double lsum = 0.0, lsq = 0.0;
     int gen = 0;
+    // Staggered start of the first tile's loads: owner w (chunk 7 - w) issues `stagger` cycles
+    // after owner w - 1, so the chunks arrive in the order the scan consumes them instead of all
+    // together at the end of the chip-wide read burst, and the scan starts under the burst.
+    if (stagger > 0 && wave > 0) {
+      const long long until = (long long)__builtin_amdgcn_s_memtime() + (long long)wave * stagger;
+      while ((long long)__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(2);
+    }
     for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
       const int n0 = pipe_tile<E>(lb, ntiles) * E;
       for (int s = 0; s < nsup; ++s) {
@@ -589,16 +596,20 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     const bool e32 = env_e == 32 ? N % 32 == 0 : (env_e == 16 ? false : (N % 32 == 0 && N / 32 >= cus));
     // DPPO_GAE_WT=0/1: plain or write-through (sc1) advantage / return stores (A/B timing)
     static const int wt = std::getenv("DPPO_GAE_WT") ? std::atoi(std::getenv("DPPO_GAE_WT")) : 0;
+    // Cycles between the owners' first load bursts: 450-750 measured 8.0-8.25 us per launch at
+    // N = 8192 against 9.1 without (1,200: 9.6, 1,800: 10.6).  DPPO_GAE_STAGGER overrides (A/B).
+    static const int stagger =
+        std::getenv("DPPO_GAE_STAGGER") ? std::atoi(std::getenv("DPPO_GAE_STAGGER")) : 640;
     const int tiles = e32 ? N / 32 : G;
     int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
     if (!e32 && grid >= 16) grid -= grid % 16;
     *n_partials = grid;
     if (e32)
       DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c, wt);
+                  adv, ret, partials, T, N, gamma, c, wt, stagger);
     else
       DPPO_LAUNCH(gae_pipe_kernel<16>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c, wt);
+                  adv, ret, partials, T, N, gamma, c, wt, stagger);
   } else if (vec)
     DPPO_LAUNCH(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
                        partials, T, N, gamma, c);
