@@ -144,13 +144,29 @@ __device__ __forceinline__ float tanh_f(float x) {
   return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
 }
 
+// Sixteen activations stage by stage: tanh = 1 - 2 / (e^{2x} + 1), five instructions each
+// (v_exp, v_rcp and three plain ones; saturates through e^{2x} = inf / 0; absolute error
+// <= ~1.2e-7), consecutive instructions independent (mbwave.hip tanh4).
 __device__ __forceinline__ void tanh_inplace(f32x16& x) {
+  float e[16];
 #pragma unroll
-  for (int r = 0; r < 16; r += 2) {
-    const f32x2 y = tanh2((f32x2){x[r], x[r + 1]});
-    x[r] = y[0];
-    x[r + 1] = y[1];
-  }
+  for (int r = 0; r < 16; ++r) e[r] = x[r] * 2.8853900817779268f;  // 2 log2(e)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(e[r]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) e[r] = e[r] + 1.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_rcpf(e[r]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) x[r] = __builtin_fmaf(-2.0f, e[r], 1.0f);
+}
+
+// part + part of lane ^ 32 with v_permlane32_swap (a VALU lane move, no LDS round trip); the
+// same two operands in both halves
+__device__ __forceinline__ float half_sum(float part) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part),
+                                                  false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
 
 // out = tanh(W X + b), W: [64][64] LDS image (stride SW), X: 2 k-blocks.
@@ -173,7 +189,9 @@ __device__ __forceinline__ void dense_tanh(f32x16 (&out)[2], const float* W, con
     }
     tanh_inplace(acc);
     out[ob] = acc;
+#ifndef DPPO_EVAL_NOFENCE
     __builtin_amdgcn_sched_barrier(0);
+#endif
   }
 }
 
@@ -225,7 +243,7 @@ __device__ __forceinline__ void heads(float (&out)[AMAX], const float* Wo, const
                   w[3] * x[fb][4 * q + 3];
         }
     }
-    out[a] = part + __shfl_xor(part, 32) + bo[a];
+    out[a] = half_sum(part) + bo[a];
   }
 }
 
@@ -241,7 +259,7 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
       part += w[0] * x[fb][4 * q + 0] + w[1] * x[fb][4 * q + 1] + w[2] * x[fb][4 * q + 2] +
               w[3] * x[fb][4 * q + 3];
     }
-  return part + __shfl_xor(part, 32) + bv;
+  return half_sum(part) + bv;
 }
 
 
