@@ -111,7 +111,8 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
-  unsigned* arrivals = nullptr;  // [4][kArrivalWords]: reduce_adam_kernel, fused tail x 2, probe
+  unsigned* arrivals = nullptr;  // [4][kArrivalWords]: (unused), fused tail x 2, probe
+  unsigned long long* ra_tags = nullptr;  // reduce_adam_kernel's tagged partials (optim.hip)
   // sticky device error word (grid_fanin timeouts): host-coherent pinned memory and its device
   // alias; the host reads it at the start of every call on the handle, without a sync
   unsigned* err_host = nullptr;
@@ -119,7 +120,7 @@ struct dppo_handle {
   unsigned long long fanin_ticks = kFaninTimeoutTicks;
   bool radam_ok = false;  // reduce_adam_kernel's grid fits on the device at once
   unsigned fused_epoch = 0;      // launches of the fused minibatch kernel with the Adam tail
-  unsigned radam_epoch = 0;      // reduce_adam launches so far on this handle
+  unsigned radam_epoch = 0;      // reduce_adam launches so far on this handle (tag of the last)
   // [E][B] permutations the minibatch kernels gather with, and the Fisher-Yates targets they are
   // resolved from (dppo_learn_targets_f32); double-buffered so the next learn's upload can run
   // on the copy stream while the current learn's minibatches still read the other buffer
@@ -218,6 +219,13 @@ int validate_dims(const dppo_dims* d) {
     return DPPO_EINVAL;
   }
   return DPPO_OK;
+}
+
+// Tag of the next reduce_adam launch: never 0, the value the tag words start from.  Every launch
+// rewrites every word, so after a wrap the words hold the previous launch's tag, not a stale match.
+unsigned next_radam_epoch(dppo_handle* h) {
+  if (++h->radam_epoch == 0u) h->radam_epoch = 1u;
+  return h->radam_epoch;
 }
 
 template <typename T>
@@ -645,9 +653,10 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
         const int Gr = G;
 #endif
         DPPO_TRY(launch_reduce_adam(
-            h->slabs, Gr, h->slab_stride, h->layout.total, h->grad, h->sq_part, h->po.ls,
-            d.continuous ? d.act_dim : 0, hp->entropy_beta, d.continuous ? 1 : 0, h->arrivals,
-            ++h->radam_epoch, params, adam_m, adam_v, hp->grad_norm_clip, (float)(-step_size), (float)bc2_sqrt,
+            h->slabs, Gr, h->slab_stride, h->layout.total, h->grad, h->ra_tags, h->po.ls,
+            d.continuous ? d.act_dim : 0, hp->entropy_beta, d.continuous ? 1 : 0,
+            next_radam_epoch(h), params, adam_m, adam_v, hp->grad_norm_clip, (float)(-step_size),
+            (float)bc2_sqrt,
             hp->adam_beta1, hp->adam_beta2, hp->adam_eps, trace, inv_m, hp->value_loss_weight,
             hp->entropy_beta, h->err_dev, h->fanin_ticks, s));
         continue;
@@ -754,6 +763,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->dsum, 4));
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
   chk(dalloc(&h->arrivals, 4 * kArrivalWords));
+  chk(dalloc(&h->ra_tags, reduce_adam_tag_words(h->layout.total)));
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->pe));
     chk(dalloc(&h->targets_dev2[k], E * h->pe));
@@ -787,7 +797,8 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   // The single-device optimizer step waits in a grid-wide fan-in: take it only when its whole
   // grid fits on the device at once (a partitioned device or an occupancy surprise takes the
   // three-kernel path -- slab reduce, clip + Adam -- instead, which needs no co-residency).
-  h->radam_ok = reduce_adam_capacity(device) >= reduce_adam_blocks(h->layout.total);
+  h->radam_ok =
+      reduce_adam_capacity(device, h->layout.total) >= reduce_adam_blocks(h->layout.total);
   for (int k = 0; k < 2 && rc == DPPO_OK; ++k) {
     hipError_t e = hipHostMalloc((void**)&h->perms_pinned[k],
                                  (size_t)(E * h->pe) * sizeof(int32_t), hipHostMallocDefault);
@@ -804,6 +815,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
     (void)hipMemset(h->trace, 0, (size_t)E * M * DPPO_TRACE_FIELDS * sizeof(float));
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
     (void)hipMemset(h->arrivals, 0, 4 * kArrivalWords * sizeof(unsigned));
+    (void)hipMemset(h->ra_tags, 0, reduce_adam_tag_words(h->layout.total) * sizeof(uint64_t));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }
@@ -845,6 +857,7 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->dsum);
   (void)hipFree(h->sq_part);
   (void)hipFree(h->arrivals);
+  (void)hipFree(h->ra_tags);
   for (int k = 0; k < 2; ++k) {
     (void)hipFree(h->perms_dev2[k]);
     (void)hipFree(h->targets_dev2[k]);

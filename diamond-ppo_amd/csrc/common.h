@@ -247,18 +247,20 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
                             const double* sq_part, int n_sq, float max_norm, float neg_step_size,
                             float bc2_sqrt, float beta1, float beta2, float eps, float* out_norm,
                             float* trace, float inv_m, float vf, float ent, hipStream_t s);
-// slab reduce + clip + Adam fused (single device): `arrivals` = a device counter zeroed once;
-// launch number `epoch` (1, 2, ...) on it waits for epoch x blocks arrivals.  On a fan-in timeout
-// (grid_fanin) the blocks leave their parameters untouched and set *err.
+// slab reduce + clip + Adam fused (single device): `tags` = reduce_adam_tag_words(p_total)
+// 64-bit words zeroed once; launch number `epoch` (1, 2, ...) publishes and waits for words
+// tagged `epoch`.  On a wait timeout the blocks leave their parameters untouched and set *err.
 int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p_total, float* grad,
-                       double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
-                       int add_entropy_const, unsigned* arrivals, unsigned epoch, float* params,
+                       unsigned long long* tags, int64_t ls_off, int ls_n, float ent_coef,
+                       int add_entropy_const, unsigned epoch, float* params,
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
                        float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s);
-// Workgroups of reduce_adam_kernel that fit on the device at once (occupancy x CUs).
-int reduce_adam_capacity(int device);
+// Workgroups of reduce_adam_kernel that fit on the device at once (occupancy x CUs; 0 when the
+// layout has more tagged words than the kernel's polling wave holds).
+int reduce_adam_capacity(int device, int64_t p_total);
 int reduce_adam_blocks(int64_t p_total);
+int reduce_adam_tag_words(int64_t p_total);
 // Fan-in self test (dppo_fanin_selftest): `blocks` workgroups of 1024 threads holding
 // `lds_bytes` of LDS each meet in one grid_fanin on `ctr` (zeroed by the caller, epoch 1).
 int launch_fanin_probe(int blocks, int lds_bytes, unsigned* ctr, unsigned* err,

@@ -189,9 +189,7 @@ __device__ __forceinline__ void dense_tanh(f32x16 (&out)[2], const float* W, con
     }
     tanh_inplace(acc);
     out[ob] = acc;
-#ifndef DPPO_EVAL_NOFENCE
     __builtin_amdgcn_sched_barrier(0);
-#endif
   }
 }
 

@@ -21,6 +21,16 @@ namespace dppo {
 namespace {
 
 constexpr int kRedParams = 64;  // parameters per slab_reduce workgroup
+
+#ifdef DPPO_RA_TRACE
+// per block of reduce_adam_kernel: s_memrealtime at entry, slabs summed, published, released, end
+__device__ long long g_ra_edges[512][5];
+#define RA_EDGE(i) \
+  if (threadIdx.x == 0 && blockIdx.x < 512) \
+    g_ra_edges[blockIdx.x][i] = (long long)__builtin_amdgcn_s_memrealtime()
+#else
+#define RA_EDGE(i)
+#endif
 constexpr int kRedWaves = 16;
 constexpr int kRedThreads = kRedWaves * 64;
 
@@ -138,63 +148,95 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(
 }
 
 // Slab reduction + clip_grad_norm_ + Adam in ONE launch (single device).  Every block reduces its
-// 64 parameters as slab_reduce_kernel does and publishes them and its sum of squares
-// write-through (sc1 stores, the storing wave drained); then all blocks meet in a grid-wide
-// fan-in (grid_fanin, common.h: monotonic counters, launch `epoch` waits for epoch x gridDim
-// arrivals, so they are never reset), each sums the per-block squares in a fixed order and
-// applies Adam to its own 64 parameters, whose gradients it still holds in registers and whose
-// moments it prefetched before the wait.  Co-residency of the ~210 blocks of 1024 threads is
-// checked once per handle (reduce_adam_capacity; a device that cannot hold them all takes the
-// three-kernel path instead), and the wait is bounded: a block whose fan-in times out leaves its
-// parameters untouched and raises the handle's sticky error word, which the next C-ABI call
-// reports -- never a silently stale norm.  (cdna_hip_programming.md Guideline 16 R1;
-// MI355X_MICROARCH.md price list: fanin vs boundary.)
+// 64 parameters as slab_reduce_kernel does, then wave 0 publishes the block's sum of squares as
+// one tagged 64-bit word {launch epoch, float partial} (the block covering the loss slots also
+// publishes those three sums the same way) and polls every block's word until all carry this
+// launch's epoch: the data is its own arrival flag, so the wait costs no counter atomics, no
+// release word and no second round trip to fetch the partials (tools/ra_trace.py: the counter
+// fan-in took ~1.7 us from publish to release, the reads after it ~0.5 us more).  Every block then
+// sums the same partials in the same order (bit-reproducible global norm) and applies Adam to its
+// own 64 parameters, whose gradients it still holds in registers and whose moments it prefetched
+// before the wait; the other 15 waves leave once the slabs are summed.  Words are read and written
+// with agent-scope atomics (sc1: no stale L2 line, no acquire fence).  Tags are monotonic per
+// handle (launch `epoch` >= 1, words zeroed at handle creation), so nothing is reset.
+// Co-residency of the ~210 blocks of 1024 threads is checked once per handle
+// (reduce_adam_capacity; a device that cannot hold them all takes the three-kernel path instead),
+// and the wait is bounded: a block whose wait times out leaves its parameters untouched and raises
+// the handle's sticky error word, which the next C-ABI call reports -- never a silently stale norm.
+constexpr int kTagWordsPerLane = 16;  // tagged words a polling lane holds: blocks + 3 <= 1024
+
+__device__ __forceinline__ unsigned long long tag_word(unsigned epoch, float x) {
+  return ((unsigned long long)epoch << 32) | __float_as_uint(x);
+}
+
 __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     const float* __restrict__ slabs, int G, int64_t stride, int64_t p_total, float* grad,
-    double* sq_part, int64_t ls_off, int ls_n, float ent_coef, int add_entropy_const,
-    unsigned* arrivals, unsigned epoch, float* __restrict__ params, float* __restrict__ m,
+    unsigned long long* tags, int64_t ls_off, int ls_n, float ent_coef, int add_entropy_const,
+    unsigned epoch, float* __restrict__ params, float* __restrict__ m,
     float* __restrict__ v, float max_norm, float neg_step_size, float bc2_sqrt, float beta1,
     float beta2, float eps, float* __restrict__ trace, float inv_m, float vf, float ent,
     unsigned* err, unsigned long long timeout_ticks) {
 #pragma clang fp contract(off)
   __shared__ float part[kRedWaves][kRedParams];
-  __shared__ int released;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t p = (int64_t)blockIdx.x * kRedParams + lane;
   const int64_t n = p_total + 8;
+  const int nb = (int)gridDim.x, nw = nb + 3;  // words: one per block, then the 3 loss sums
   // this block's Adam operands, loaded while the slabs stream in
   float mk = 0.f, vk = 0.f, pk = 0.f;
+  RA_EDGE(0);
   if (wave == 0 && p < p_total) {
     mk = m[p];
     vk = v[p];
     pk = params[p];
   }
   float t = slab_sum(slabs, G, stride, p, n, part);
-  if (wave == 0) {
-    if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
-    if (p < n) __hip_atomic_store(grad + p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    double q = (p < p_total) ? (double)t * (double)t : 0.0;
-    for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
-    if (lane == 0)
-      __hip_atomic_store(sq_part + blockIdx.x, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains (R1)
+  RA_EDGE(1);
+  if (wave != 0) return;
+  if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
+  if (p < n) grad[p] = t;
+  double q = (p < p_total) ? (double)t * (double)t : 0.0;
+  for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+  if (lane == 0)
+    __hip_atomic_store(tags + blockIdx.x, tag_word(epoch, (float)q), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (p >= p_total && p < p_total + 3)
+    __hip_atomic_store(tags + nb + (p - p_total), tag_word(epoch, t), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  RA_EDGE(2);
+  // poll: each lane keeps its words' loads in flight together; the loop exit is wave-uniform
+  unsigned long long w[kTagWordsPerLane];
+  unsigned pending = 0;
+#pragma unroll
+  for (int j = 0; j < kTagWordsPerLane; ++j) {
+    w[j] = 0;
+    if (j * 64 + lane < nw) pending |= 1u << j;
   }
-  __syncthreads();
-  // Fan-in sharded by XCD group (blockIdx % 8, one XCD under round-robin dispatch; any placement
-  // is correct): ~G/8 arrivals per counter instead of G serialised atomics on one word (~13 ns
-  // each, MI355X_MICROARCH.md fanin); the waiters poll a separate release word, so their loads
-  // never queue in front of the arrival atomics.
-  if (threadIdx.x == 0) released = grid_fanin(arrivals, epoch, timeout_ticks, err) ? 1 : 0;
-  __syncthreads();
-  if (wave != 0 || !released) return;
-  // Everything read below that other blocks wrote (sq_part, the loss slots) is read with sc1
-  // (agent-scope atomic) loads, so no acquire fence (and its L1 invalidate, ~1.5 us per CU) is
-  // needed: producer sc1 stores -> vmcnt(0) -> arrival; consumer sees the count -> sc1 loads
-  // (cdna_hip_programming.md Guideline 16 R1, condition 4).
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned k = 0;; ++k) {
+#pragma unroll
+    for (int j = 0; j < kTagWordsPerLane; ++j)
+      if (pending & (1u << j))
+        w[j] = __hip_atomic_load(tags + j * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int j = 0; j < kTagWordsPerLane; ++j)
+      if ((unsigned)(w[j] >> 32) == epoch) pending &= ~(1u << j);
+    if (__ballot(pending != 0) == 0) break;
+    __builtin_amdgcn_s_sleep(1);
+    if ((k & 255u) == 255u) {
+      const bool late = __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks;
+      if (late || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        __hip_atomic_store(err, kErrFaninTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;  // parameters untouched; the next C-ABI call reports the error
+      }
+    }
+  }
+  RA_EDGE(3);
   // global norm: every block sums the same per-block squares in the same order
   double sq = 0.0;
-  for (int k = lane; k < (int)gridDim.x; k += 64)
-    sq += __hip_atomic_load(sq_part + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int j = 0; j < kTagWordsPerLane; ++j)
+    if (j * 64 + lane < nb) sq += (double)__uint_as_float((unsigned)w[j]);
   for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
   float norm;
   const float coef = clip_coef(sq, max_norm, &norm);
@@ -205,12 +247,23 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     m[p] = mk;
     v[p] = vk;
   }
-  // the loss slots (published by the block past the last parameter) for the trace
-  if (blockIdx.x == 0 && lane == 0 && trace) {
-    const float s_pi = __hip_atomic_load(grad + p_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float s_v = __hip_atomic_load(grad + p_total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float s_h = __hip_atomic_load(grad + p_total + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    write_trace(trace, s_pi, s_v, s_h, norm, inv_m, vf, ent);
+#ifdef DPPO_RA_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  RA_EDGE(4);
+#endif
+  if (blockIdx.x == 0 && trace) {
+    // the loss sums: words nb .. nb + 2 (lane (nb + i) % 64, slot (nb + i) / 64)
+    float s[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int wi = nb + i, ji = wi >> 6;
+      float x = 0.f;
+#pragma unroll
+      for (int j = 0; j < kTagWordsPerLane; ++j)
+        if (j == ji) x = __uint_as_float((unsigned)w[j]);
+      s[i] = __shfl(x, wi & 63);
+    }
+    if (lane == 0) write_trace(trace, s[0], s[1], s[2], norm, inv_m, vf, ent);
   }
 }
 
@@ -238,6 +291,12 @@ __global__ __launch_bounds__(256) void rank_sum_kernel(RankPtrs src, int n, F* _
 }
 
 }  // namespace
+
+#ifdef DPPO_RA_TRACE
+extern "C" __attribute__((visibility("default"))) int dppo_debug_ra_edges(long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ra_edges), sizeof(g_ra_edges)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int launch_rank_sum(const RankPtrs& src, int n, void* out, int64_t count, bool f64,
                     hipStream_t s) {
@@ -281,14 +340,14 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
 }
 
 int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p_total, float* grad,
-                       double* sq_part, int64_t ls_off, int ls_n, float ent_coef,
-                       int add_entropy_const, unsigned* arrivals, unsigned epoch, float* params,
+                       unsigned long long* tags, int64_t ls_off, int ls_n, float ent_coef,
+                       int add_entropy_const, unsigned epoch, float* params,
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
                        float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s) {
   DPPO_LAUNCH(reduce_adam_kernel, dim3(reduce_adam_blocks(p_total)), dim3(kRedThreads), 0, s, slabs, G,
-              slab_stride, p_total, grad, sq_part, ls_off, ls_n, ent_coef, add_entropy_const,
-              arrivals, epoch, params, m, v, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
+              slab_stride, p_total, grad, tags, ls_off, ls_n, ent_coef, add_entropy_const,
+              epoch, params, m, v, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
               trace, inv_m, vf, ent, err, timeout_ticks);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
@@ -296,7 +355,10 @@ int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p
 
 int reduce_adam_blocks(int64_t p_total) { return slab_reduce_blocks(p_total); }
 
-int reduce_adam_capacity(int device) {
+int reduce_adam_tag_words(int64_t p_total) { return reduce_adam_blocks(p_total) + 3; }
+
+int reduce_adam_capacity(int device, int64_t p_total) {
+  if (reduce_adam_tag_words(p_total) > 64 * kTagWordsPerLane) return 0;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)reduce_adam_kernel,
                                                    kRedThreads, 0) != hipSuccess ||
