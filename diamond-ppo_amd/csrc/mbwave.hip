@@ -182,14 +182,24 @@ __device__ __forceinline__ float tanh_w(float x) {
   return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
 
-// Sixteen activations stage by stage (all multiplies, all exps, ...): consecutive instructions are
-// independent, so that pinned between MFMAs each issue slot holds work that is ready.
+// The hidden layers' weights and biases are staged into LDS pre-multiplied by kTS = 2 log2(e),
+// so a layer's MFMAs produce kTS z directly and its tanh needs no multiply (4 VALU instructions
+// per activation instead of 5: on gfx950 fp32 MFMA work every VALU instruction costs its issue
+// slot).  The backward pass runs through the same scaled images: dh2 comes out
+// kTS-scaled and dh1 kTS^2-scaled, so the W2 / b2 gradients carry kTS and W1 / b1 kTS^2, undone
+// once per launch in the epilogue (a few ulp against the unscaled products; the parity bounds
+// are 2e-5 of the gradient scale).
+constexpr float kTS = 2.8853900817779268f;
+constexpr float kInvTS = 1.0f / kTS;
+constexpr float kInvTS2 = 1.0f / (kTS * kTS);
+
+// Sixteen activations stage by stage (all exps, all adds, ...) from pre-scaled inputs kTS z:
+// consecutive instructions are independent, so that pinned between MFMAs each issue slot holds
+// work that is ready.
 __device__ __forceinline__ void tanh4(f32x4 (&y)[4]) {
   float e[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) e[i] = y[i >> 2][i & 3] * 2.8853900817779268f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
+  for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(y[i >> 2][i & 3]);
 #pragma unroll
   for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
 #pragma unroll
@@ -484,22 +494,22 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   for (int i = 0; i < kWLd; ++i) {
     const int k = tid + i * kThreadsW;
     const int mi = k >> 10, e = k & 1023, row = e >> 4, g = e & 15;
-    *(f32x4*)(lds + L.W2 + mi * H * kWS + row * kWS + 4 * g) = wld[i];
+    *(f32x4*)(lds + L.W2 + mi * H * kWS + row * kWS + 4 * g) = wld[i] * kTS;
   }
 #pragma unroll
   for (int i = 0; i < kW1Ld; ++i) {
     const int k = tid + i * kThreadsW;
     const int row = k / L.RS1, c = k - row * L.RS1;
-    if (k < H * L.RS1) lds[L.W1 + k] = c < D ? w1ld[i] : 0.0f;
+    if (k < H * L.RS1) lds[L.W1 + k] = c < D ? w1ld[i] * kTS : 0.0f;
   }
   lds[L.Wo + tid] = (tid >> 6) < a.A ? wold : 0.0f;
   lds[L.Wo + 4 * H + tid] = (tid >> 6) + 4 < a.A ? wold2 : 0.0f;
   if (tid < H) {
     lds[L.Wv + tid] = P[po.Wv + tid];
-    lds[L.b1 + tid] = P[po.b1 + tid];
-    lds[L.b2 + tid] = P[po.b2 + tid];
-    lds[L.ba + tid] = P[po.ba + tid];
-    lds[L.bc + tid] = P[po.bc + tid];
+    lds[L.b1 + tid] = P[po.b1 + tid] * kTS;
+    lds[L.b2 + tid] = P[po.b2 + tid] * kTS;
+    lds[L.ba + tid] = P[po.ba + tid] * kTS;
+    lds[L.bc + tid] = P[po.bc + tid] * kTS;
   } else if (tid < H + 8) {
     const int h = tid - H;
     lds[L.bo + h] = h < a.A ? P[po.bo + h] : 0.0f;
@@ -826,12 +836,12 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         }
       }
   };
-  auto sum_mat = [&](const float* stg, int64_t off, int n4) {
+  auto sum_mat = [&](const float* stg, int64_t off, int n4, float scale) {
     for (int c = tid; c < n4; c += kThreadsW) {
       const f32x4 v = ((((const f32x4*)stg)[c] + ((const f32x4*)(stg + kMat))[c]) +
                        ((const f32x4*)(stg + 2 * kMat))[c]) +
                       ((const f32x4*)(stg + 3 * kMat))[c];
-      slab_st4(slab + off + 4 * c, v);
+      slab_st4(slab + off + 4 * c, scale == 1.0f ? v : v * scale);
     }
   };
   // register-only reductions of this wave's small items first (they overlap the wait for the
@@ -887,15 +897,15 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   ESTAMP(1);
   __syncthreads();
   ESTAMP(2);
-  sum_mat(stg0, po.W2, kMat / 4);
-  sum_mat(stg1, po.Wa, kMat / 4);
+  sum_mat(stg0, po.W2, kMat / 4, kInvTS);
+  sum_mat(stg1, po.Wa, kMat / 4, 1.0f);
   for (int j = tid; j < kSmallW; j += kThreadsW) {
     const float v = ((small[j] + small[kSmallW + j]) + small[2 * kSmallW + j]) +
                     small[3 * kSmallW + j];
     if (j < 4 * H) {
       const int l = j >> 6, f = j & 63;
       const int64_t off = l == 0 ? po.b1 : (l == 1 ? po.b2 : (l == 2 ? po.ba : po.bc));
-      slab[off + f] = v;
+      slab[off + f] = l == 0 ? v * kInvTS2 : (l == 1 ? v * kInvTS : v);
     } else if (j < (4 + AMAX) * H) {
       const int h = (j - 4 * H) >> 6, f = j & 63;
       if (h < a.A) slab[po.Wo + h * H + f] = v;
@@ -921,8 +931,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   ESTAMP(4);
   __syncthreads();
   ESTAMP(5);
-  sum_mat(stg0, po.Wc, kMat / 4);
-  sum_mat(stg1, po.W1, H * D / 4);
+  sum_mat(stg0, po.Wc, kMat / 4, 1.0f);
+  sum_mat(stg1, po.W1, H * D / 4, kInvTS2);
   ESTAMP(6);
 #ifdef DPPO_PHASE_TRACE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
