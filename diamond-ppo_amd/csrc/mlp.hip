@@ -30,6 +30,10 @@ constexpr int SW = H + 4;  // LDS row stride (floats) of the H-wide weight image
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / kWave;
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
+// Hidden-layer weights and biases are staged into LDS pre-multiplied by kTS = 2 log2(e): the
+// MFMAs then produce kTS z and tanh_inplace skips its multiply (one VALU instruction fewer per
+// activation; VALU is not hidden behind fp32 MFMAs on gfx950).
+constexpr float kTS = 2.8853900817779268f;
 
 struct LdsLayout {
   int W1, S1;          // W1 image [H][S1], S1 = D8 + 4 (zero-padded columns D..S1)
@@ -99,21 +103,21 @@ __device__ __forceinline__ void load_weights(float* lds, const KArgs& a, int tid
   const LdsLayout& L = a.L;
   for (int k = tid; k < H * L.S1; k += kThreads) {
     const int o = k / L.S1, c = k % L.S1;
-    lds[L.W1 + k] = c < a.D ? P[a.po.W1 + o * a.D + c] : 0.0f;
+    lds[L.W1 + k] = c < a.D ? P[a.po.W1 + o * a.D + c] * kTS : 0.0f;
   }
   for (int k = tid; k < H * H; k += kThreads) {
     const int o = k >> 6, c = k & 63;
-    lds[L.W2 + o * SW + c] = P[a.po.W2 + k];
-    lds[L.Wa + o * SW + c] = P[a.po.Wa + k];
-    lds[L.Wc + o * SW + c] = P[a.po.Wc + k];
+    lds[L.W2 + o * SW + c] = P[a.po.W2 + k] * kTS;
+    lds[L.Wa + o * SW + c] = P[a.po.Wa + k] * kTS;
+    lds[L.Wc + o * SW + c] = P[a.po.Wc + k] * kTS;
   }
   for (int k = tid; k < a.A * H; k += kThreads) lds[L.Wo + k] = P[a.po.Wo + k];
   for (int k = tid; k < H; k += kThreads) {
     lds[L.Wv + k] = P[a.po.Wv + k];
-    lds[L.b1 + k] = P[a.po.b1 + k];
-    lds[L.b2 + k] = P[a.po.b2 + k];
-    lds[L.ba + k] = P[a.po.ba + k];
-    lds[L.bc + k] = P[a.po.bc + k];
+    lds[L.b1 + k] = P[a.po.b1 + k] * kTS;
+    lds[L.b2 + k] = P[a.po.b2 + k] * kTS;
+    lds[L.ba + k] = P[a.po.ba + k] * kTS;
+    lds[L.bc + k] = P[a.po.bc + k] * kTS;
   }
   for (int k = tid; k < 32; k += kThreads) {
     lds[L.bo + k] = k < a.A ? P[a.po.bo + k] : 0.0f;
@@ -137,22 +141,13 @@ __device__ __forceinline__ f32x16 bias_block(const float* b, int ob, int h) {
   return acc;
 }
 
-// tanh = sign(x) (1 - t) / (1 + t), t = e^{-2|x|}: one exp, one hardware reciprocal, branch-free
-// (absolute error <= ~1.5e-7; mbstep.hip uses the same form).
-__device__ __forceinline__ float tanh_f(float x) {
-  const float t = __expf(-2.0f * fabsf(x));
-  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
-}
-
-// Sixteen activations stage by stage: tanh = 1 - 2 / (e^{2x} + 1), five instructions each
-// (v_exp, v_rcp and three plain ones; saturates through e^{2x} = inf / 0; absolute error
-// <= ~1.2e-7), consecutive instructions independent (mbwave.hip tanh4).
+// Sixteen activations stage by stage from pre-scaled inputs x = kTS z: tanh z = 1 - 2 / (2^x + 1),
+// four instructions each (v_exp, v_rcp and two plain ones; saturates through 2^x = inf / 0;
+// absolute error <= ~1.2e-7), consecutive instructions independent (mbwave.hip tanh4).
 __device__ __forceinline__ void tanh_inplace(f32x16& x) {
   float e[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) e[r] = x[r] * 2.8853900817779268f;  // 2 log2(e)
-#pragma unroll
-  for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(e[r]);
+  for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(x[r]);
 #pragma unroll
   for (int r = 0; r < 16; ++r) e[r] = e[r] + 1.0f;
 #pragma unroll
@@ -399,18 +394,18 @@ __device__ __forceinline__ void load_weights_actor(float* lds, const ActArgs& a,
   const LdsLayout& L = a.L;
   for (int k = tid; k < H * L.S1; k += kThreads) {
     const int o = k / L.S1, c = k % L.S1;
-    lds[L.W1 + k] = c < a.D ? P[a.po.W1 + o * a.D + c] : 0.0f;
+    lds[L.W1 + k] = c < a.D ? P[a.po.W1 + o * a.D + c] * kTS : 0.0f;
   }
   for (int k = tid; k < H * H; k += kThreads) {
     const int o = k >> 6, c = k & 63;
-    lds[L.W2 + o * SW + c] = P[a.po.W2 + k];
-    lds[L.Wa + o * SW + c] = P[a.po.Wa + k];
+    lds[L.W2 + o * SW + c] = P[a.po.W2 + k] * kTS;
+    lds[L.Wa + o * SW + c] = P[a.po.Wa + k] * kTS;
   }
   for (int k = tid; k < a.A * H; k += kThreads) lds[L.Wo + k] = P[a.po.Wo + k];
   for (int k = tid; k < H; k += kThreads) {
-    lds[L.b1 + k] = P[a.po.b1 + k];
-    lds[L.b2 + k] = P[a.po.b2 + k];
-    lds[L.ba + k] = P[a.po.ba + k];
+    lds[L.b1 + k] = P[a.po.b1 + k] * kTS;
+    lds[L.b2 + k] = P[a.po.b2 + k] * kTS;
+    lds[L.ba + k] = P[a.po.ba + k] * kTS;
   }
   for (int k = tid; k < 32; k += kThreads) {
     lds[L.bo + k] = k < a.A ? P[a.po.bo + k] : 0.0f;
