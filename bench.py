@@ -243,7 +243,7 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
     def timed_pass(instrument: bool):
         """K learns between barrier + synchronize brackets; max wall time over ranks."""
         h.set_timing(instrument)
-        for k in ("perms", "enqueue", "draft_start"):
+        for k in ("perms", "enqueue", "draft_start", "draw", "slot_wait"):
             hs[k] = 0.0
         hs["calls"] = 0
         hs["lookahead_hits"] = 0
@@ -266,7 +266,8 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
     # Pass A (the reported throughput): no per-launch events in the stream.
     elapsed = timed_pass(False)
     host = {k: round(hs[k] / max(hs["calls"], 1) * 1e3, 4) for k in ("perms", "enqueue",
-                                                                      "draft_start")}
+                                                                      "draft_start", "draw",
+                                                                      "slot_wait")}
     hits = hs["lookahead_hits"]
     # Pass B (the per-kernel table and the roofline): the same K learns with the kernels' own
     # start/end HIP events (libdppo timing mode); never the throughput.
@@ -330,6 +331,9 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "instrumented_ms_per_step": (round(elapsed_instr / steps * 1e3, 4)
                                      if elapsed_instr else None),
         "host_ms_per_step": host,
+        # the host's own work per learn (draws on the draft thread + the launching thread's
+        # calls), excluding time spent blocked on the device
+        "host_work_ms_per_step": round(host["draw"] + host["enqueue"] + host["draft_start"], 4),
         "perm_lookahead_hits": hits,
         "final_loss": float(loss_trace[-1, 0]),
     }
@@ -398,7 +402,8 @@ def main():
                 continue
             r = run_config(name, 1, 0, None, device, min(args.steps, 10), 2)
             extra[name] = {k: r[k] for k in ("value", "ms_per_step", "update_steps_per_s",
-                                             "device_ms_per_step", "host_ms_per_step")}
+                                             "device_ms_per_step", "host_ms_per_step",
+                                             "host_work_ms_per_step")}
             extra[name]["roofline"] = r["roofline"]
             extra[name]["config"] = r["config"]
         out["configs_extra"] = extra

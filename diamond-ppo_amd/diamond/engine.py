@@ -349,10 +349,12 @@ class NativeLearner:
         if self.world > 1:
             self._init_comm()
         self.last_trace = None
-        # host-side seconds per phase of learn() (swap targets incl. waiting for the look-ahead
-        # draft, native enqueue, starting the next draft) -- reported by bench.py
-        self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "calls": 0,
-                             "lookahead_hits": 0}
+        # host-side seconds of learn(), reported by bench.py.  Launching thread: "perms" (waiting
+        # for the look-ahead draft, which includes its wait for a free pinned slot), "draft_start"
+        # and "enqueue" (the native learn call).  Draft thread: "draw" (the permutation draws
+        # themselves: the host's own work per learn) and "slot_wait" (device back-pressure).
+        self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "draw": 0.0,
+                             "slot_wait": 0.0, "calls": 0, "lookahead_hits": 0}
         self.lookahead = os.environ.get("DPPO_PERM_LOOKAHEAD", "1") != "0"
         # Where the Fisher-Yates swaps run.  The host's swap chain is cache-miss bound once the
         # [E][B] permutations outgrow the caches (C5 on one GPU, E*B = 33.5 M: ~46 ms of host
@@ -412,18 +414,23 @@ class NativeLearner:
         return out.copy() if self.continuous else out.astype(np.int64)
 
     def _start_draft(self, key: np.ndarray, pos: int):
-        """Draw the next learn's permutations (or swap targets) on the draft worker thread."""
+        """Draw the next learn's permutations (or swap targets) on the draft worker thread.
+        The worker first waits until the pinned slot's previous upload is done (device
+        back-pressure), so the launching thread never blocks here."""
         slot = 1 - self._slot
-        buf = self.handle.perm_buffer(slot)
-        d = {"slot": slot, "buf": buf, "key_in": key.copy(), "pos_in": pos, "ok": False,
+        d = {"slot": slot, "key_in": key.copy(), "pos_in": pos, "ok": False,
              "device": self.device_shuffle, "done": threading.Event()}
 
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
 
         def work():
+            t0 = time.perf_counter()
+            d["buf"] = buf = self.handle.perm_buffer(slot)
+            t1 = time.perf_counter()
             k = d["key_in"].copy()
             d["pos_out"] = draw(k, d["pos_in"], self.perm_n, self.cfg.num_epochs, buf)
             d["key_out"] = k
+            d["t_slot"], d["t_draw"] = t1 - t0, time.perf_counter() - t1
             d["ok"] = True
 
         if self._worker is None:
@@ -439,6 +446,9 @@ class NativeLearner:
         d, self._draft = self._draft, None
         if d is not None:
             d["done"].wait()
+            if d["ok"]:
+                self.host_seconds["draw"] += d["t_draw"]
+                self.host_seconds["slot_wait"] += d["t_slot"]
             if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos
                     and np.array_equal(d["key_in"], key)):
                 self._slot = d["slot"]
@@ -447,7 +457,9 @@ class NativeLearner:
                 return d["buf"], d["key_out"], d["pos_out"]
         buf = self.handle.perm_buffer(self._slot)
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
+        t0 = time.perf_counter()
         pos = draw(key, pos, self.perm_n, self.cfg.num_epochs, buf)
+        self.host_seconds["draw"] += time.perf_counter() - t0
         N.set_mt_state(st, key, pos)
         return buf, key, pos
 

@@ -15,14 +15,16 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 524288
 E = 4
 out = np.empty(E * n, np.int32)
 np.random.seed(42)
-for name, fn in (("perm_numpy", N.perm_numpy), ("perm_targets_numpy", N.perm_targets_numpy)):
-    ts = []
-    for _ in range(5):
-        key, pos, _ = N.mt_state()
-        t0 = time.perf_counter()
-        fn(key, pos, n, E, out)
-        ts.append(time.perf_counter() - t0)
-    print(f"{name}: {min(ts) * 1e3:.2f} ms (min of 5), {E}x{n}")
+for cnt in (1, 2, E):
+    for name, fn in (("perm_numpy", N.perm_numpy), ("perm_targets_numpy", N.perm_targets_numpy)):
+        ts = []
+        for _ in range(7):
+            key, pos, _ = N.mt_state()
+            t0 = time.perf_counter()
+            fn(key, pos, n, cnt, out)
+            ts.append(time.perf_counter() - t0)
+        print(f"{name}: {min(ts) * 1e3:.3f} ms (min of 7), median {np.median(ts) * 1e3:.3f}, "
+              f"{cnt}x{n}")
 t0 = time.perf_counter()
 for _ in range(E):
     np.random.permutation(n)
