@@ -210,7 +210,10 @@ __device__ __forceinline__ void gae_terms(float r, float v, float nv, float te, 
 // instead of as a dirty line written back at the kernel boundary (MI355X_MICROARCH.md
 // publish-large / boundary: a predecessor leaving B dirty bytes costs ~B / 6 TB/s)
 __device__ __forceinline__ void store_wt(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  // s_nop: a VALU write to the data VGPRs of a store wider than 8 bytes needs a wait state
+  // after it, which the compiler cannot insert behind an asm statement (seen: back-to-back slab
+  // stores whose next operands overwrote this one's data before it was read)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ float gae_carry(float delta, float coef, float a) {

@@ -291,7 +291,10 @@ __device__ __forceinline__ void slab_put4(float* p, f32x4 v) {
 #ifdef DPPO_ABL_PLAINSLAB
   *(f32x4*)p = v;
 #else
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  // s_nop: a VALU write to the data VGPRs of a store wider than 8 bytes needs a wait state
+  // after it, which the compiler cannot insert behind an asm statement (seen: back-to-back slab
+  // stores whose next operands overwrote this one's data before it was read)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 #endif
 }
 

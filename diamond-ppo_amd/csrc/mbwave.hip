@@ -380,7 +380,10 @@ __device__ __forceinline__ void get_n(f32x4 (&n)[4], const float* sm, int q, int
 }
 
 __device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  // s_nop: a VALU write to the data VGPRs of a store wider than 8 bytes needs a wait state
+  // after it, which the compiler cannot insert behind an asm statement (seen: back-to-back slab
+  // stores whose next operands overwrote this one's data before it was read)
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ f32x4 z4() { return (f32x4){0.f, 0.f, 0.f, 0.f}; }
@@ -844,6 +847,20 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       slab_st4(slab + off + 4 * c, scale == 1.0f ? v : v * scale);
     }
   };
+  // a whole hidden matrix: all sixteen LDS reads of a thread in flight before the first add
+  auto sum_hid = [&](const float* stg, int64_t off, float scale) {
+    constexpr int kIt = kMat / 4 / kThreadsW;
+    f32x4 x[kIt][4];
+#pragma unroll
+    for (int i = 0; i < kIt; ++i)
+#pragma unroll
+      for (int w = 0; w < 4; ++w) x[i][w] = ((const f32x4*)(stg + w * kMat))[tid + i * kThreadsW];
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) {
+      const f32x4 v = ((x[i][0] + x[i][1]) + x[i][2]) + x[i][3];
+      slab_st4(slab + off + 4 * (tid + i * kThreadsW), scale == 1.0f ? v : v * scale);
+    }
+  };
   // register-only reductions of this wave's small items first (they overlap the wait for the
   // slowest wave): hidden biases and head weights (P form: sum over q), head biases / log-std /
   // loss sums (every lane: 16-lane rows by DPP, then the four rows)
@@ -897,8 +914,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   ESTAMP(1);
   __syncthreads();
   ESTAMP(2);
-  sum_mat(stg0, po.W2, kMat / 4, kInvTS);
-  sum_mat(stg1, po.Wa, kMat / 4, 1.0f);
+  sum_hid(stg0, po.W2, kInvTS);
+  sum_hid(stg1, po.Wa, 1.0f);
   for (int j = tid; j < kSmallW; j += kThreadsW) {
     const float v = ((small[j] + small[kSmallW + j]) + small[2 * kSmallW + j]) +
                     small[3 * kSmallW + j];
@@ -931,7 +948,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   ESTAMP(4);
   __syncthreads();
   ESTAMP(5);
-  sum_mat(stg0, po.Wc, kMat / 4, 1.0f);
+  sum_hid(stg0, po.Wc, 1.0f);
   sum_mat(stg1, po.W1, H * D / 4, kInvTS2);
   ESTAMP(6);
 #ifdef DPPO_PHASE_TRACE
