@@ -568,25 +568,37 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   WEDGE(1, (long long)__builtin_amdgcn_s_memtime());
 #endif
 
-  for (int k = 0; k < nk; ++k) {
-    const int g0 = (first + k * stride) * 16;
-    const bool valid = g0 + r < mm;
-    WSTAMP(k, 0);
-    // ---- (1) layer 1: h1 = tanh(W1 x + b1); k-step t covers inputs {4t + q}
-    f32x4 h1[4];
+  // ---- (1) layer 1: h1 = tanh(W1 x + b1); k-step t covers inputs {4t + q}.  Group k + 1's runs
+  // inside group k's last phase (its 4 MFMAs and tanh beside that phase's 80 weight-gradient
+  // MFMAs, instead of a latency-bound phase of its own), so h1 is carried across iterations.
+  auto layer1 = [&](f32x4 (&h)[4], const GRec<NIB>& g) {
 #pragma unroll
-    for (int ob = 0; ob < 4; ++ob) h1[ob] = *(const f32x4*)(lds + L.b1 + 16 * ob + 4 * q);
+    for (int ob = 0; ob < 4; ++ob) h[ob] = *(const f32x4*)(lds + L.b1 + 16 * ob + 4 * q);
 #pragma unroll
     for (int t = 0; t < 4 * NIB; ++t) {
       if (t < a.nkn) {
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob)
-          h1[ob] = mfma4(lds[L.W1 + (16 * ob + r) * L.RS1 + 4 * t + q], g_cur.xn[t], h1[ob]);
+          h[ob] = mfma4(lds[L.W1 + (16 * ob + r) * L.RS1 + 4 * t + q], g.xn[t], h[ob]);
       }
     }
-    tanh4(h1);
-    put_n(sh1, h1, q, r);
-    PHASE_FENCE();
+    tanh4(h);
+    put_n(sh1, h, q, r);
+  };
+  // (only where the registers allow it: the other instantiations would spill)
+  constexpr bool kHoistL1 = AMAX == 2 && !CONT && NIB == 1;
+  f32x4 h1[4];
+  if (kHoistL1 && nk > 0) layer1(h1, g_cur);
+  PHASE_FENCE();
+
+  for (int k = 0; k < nk; ++k) {
+    const int g0 = (first + k * stride) * 16;
+    const bool valid = g0 + r < mm;
+    WSTAMP(k, 0);
+    if (!kHoistL1) {
+      layer1(h1, g_cur);
+      PHASE_FENCE();
+    }
     WSTAMP(k, 1);
     // ---- (2) layer 2
     f32x4 h2[4];
@@ -792,6 +804,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       // dz2 again in the P layout (from the same slot) and h1 for dW2
       get_p(dz2t, sx, q, r);
       get_p(h1t, sh1, q, r);
+      // the next group's layer 1 (sh1 is free once h1t is read: one wave's LDS ops run in order)
+      if (kHoistL1 && k + 1 < nk) layer1(h1, g_nxt);
       wgrad<4>(gW2, dz2t, h1t);
       f32x4 dz1t[4];
 #pragma unroll
