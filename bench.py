@@ -333,7 +333,8 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "host_ms_per_step": host,
         # the host's own work per learn (draws on the draft thread + the launching thread's
         # calls), excluding time spent blocked on the device
-        "host_work_ms_per_step": round(host["draw"] + host["enqueue"] + host["draft_start"], 4),
+        "host_work_ms_per_step": round(host["draw"] + host["enqueue"] + host["draft_start"]
+                                       - host["slot_wait"], 4),
         "perm_lookahead_hits": hits,
         "final_loss": float(loss_trace[-1, 0]),
     }

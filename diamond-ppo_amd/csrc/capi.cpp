@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -84,6 +85,8 @@ struct LoopGroup {
     }                                                                                     \
   } while (0)
 
+constexpr int kPermSlots = DPPO_PERM_SLOTS;
+
 struct dppo_handle {
   int device = 0;
   dppo_dims dims{};
@@ -134,9 +137,10 @@ struct dppo_handle {
   hipEvent_t perms_free[2] = {nullptr, nullptr};  // the last learn reading device slot k is done
   bool perms_free_valid[2] = {false, false};
   // two pinned host staging slots, each with the event that marks its upload done
-  int32_t* perms_pinned[2] = {nullptr, nullptr};
-  hipEvent_t perm_copy_done[2] = {nullptr, nullptr};
-  bool perm_copy_pending[2] = {false, false};
+  // kPermSlots pinned host staging slots: one being uploaded, one ready, one being drawn
+  int32_t* perms_pinned[kPermSlots] = {};
+  hipEvent_t perm_copy_done[kPermSlots] = {};
+  bool perm_copy_pending[kPermSlots] = {};
   int32_t trace_rows = 0;
   hipStream_t last_stream = nullptr;
   // optional per-kernel-class timing with HIP events on the launch stream
@@ -513,7 +517,9 @@ namespace {
 // pinned slot is copied from directly (pure DMA); any other buffer is first staged in slot 0.
 int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, int ds) {
   const size_t pbytes = (size_t)(h->dims.num_epochs * h->pe) * sizeof(int32_t);
-  int slot = host == h->perms_pinned[1] ? 1 : 0;
+  int slot = 0;
+  for (int k = 1; k < kPermSlots; ++k)
+    if (host == h->perms_pinned[k]) slot = k;
   if (host != h->perms_pinned[slot]) {
     if (h->perm_copy_pending[0]) DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done[0]));
     std::memcpy(h->perms_pinned[0], host, pbytes);
@@ -799,7 +805,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   // three-kernel path -- slab reduce, clip + Adam -- instead, which needs no co-residency).
   h->radam_ok =
       reduce_adam_capacity(device, h->layout.total) >= reduce_adam_blocks(h->layout.total);
-  for (int k = 0; k < 2 && rc == DPPO_OK; ++k) {
+  for (int k = 0; k < kPermSlots && rc == DPPO_OK; ++k) {
     hipError_t e = hipHostMalloc((void**)&h->perms_pinned[k],
                                  (size_t)(E * h->pe) * sizeof(int32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -869,7 +875,7 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->perms_local);
   (void)hipFree(h->seg);
   (void)hipFree(h->sel_cnt);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kPermSlots; ++k) {
     if (h->perms_pinned[k]) (void)hipHostFree(h->perms_pinned[k]);
     if (h->perm_copy_done[k]) (void)hipEventDestroy(h->perm_copy_done[k]);
   }
@@ -1052,13 +1058,22 @@ int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t
 }
 
 int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out) {
-  if (!h || !out || slot < 0 || slot > 1) {
+  if (!h || !out || slot < 0 || slot >= kPermSlots) {
     set_error("invalid argument to dppo_perm_buffer");
     return DPPO_EINVAL;
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   if (h->perm_copy_pending[slot]) {
-    DPPO_HIP_CHECK(hipEventSynchronize(h->perm_copy_done[slot]));
+    // polled with sleeps, not hipEventSynchronize: this runs on the draft thread, where a blocking
+    // (spinning) wait slowed the launching thread's kernel enqueues ~2x (0.24 -> 0.55 ms per
+    // learn) and left gaps between the learn's kernels
+    hipError_t e;
+    while ((e = hipEventQuery(h->perm_copy_done[slot])) == hipErrorNotReady)
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    if (e != hipSuccess) {
+      set_error("hipEventQuery: %s", hipGetErrorString(e));
+      return DPPO_EHIP;
+    }
     h->perm_copy_pending[slot] = false;
   }
   *out = h->perms_pinned[slot];

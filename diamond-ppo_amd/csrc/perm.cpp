@@ -201,24 +201,17 @@ void apply_swaps(int32_t* __restrict a, const int32_t* __restrict j, int64_t n) 
   }
 }
 
-// The CPUs that share the calling thread's L3 (and that this process may run on).  The swap
-// chain of an epoch reads the targets the drawing thread just wrote: on a multi-CCD host a worker
-// in another L3 domain runs it ~3x slower (EPYC 9575F: 4 epochs 1.3 ms with the workers beside
-// the drawing thread, 3-4 ms placed freely, 2.25 ms on one thread).
-bool l3_domain(cpu_set_t* out) {
-  const int home = sched_getcpu();
-  if (home < 0) return false;
+// The allowed CPUs that share an L3 with `cpu`.
+bool l3_of(int cpu, const cpu_set_t& allowed, cpu_set_t* out) {
   char path[96];
   std::snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list",
-                home);
+                cpu);
   FILE* f = std::fopen(path, "r");
   if (!f) return false;
   char buf[512] = {0};
   const bool got = std::fgets(buf, sizeof(buf), f) != nullptr;
   std::fclose(f);
   if (!got) return false;
-  cpu_set_t allowed;
-  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
   CPU_ZERO(out);
   int count = 0;
   for (char* p = buf; *p;) {  // "a-b,c,d-e"
@@ -238,7 +231,46 @@ bool l3_domain(cpu_set_t* out) {
       }
     while (*p == ',' || *p == '\n' || *p == ' ') ++p;
   }
-  return count >= 2 && CPU_ISSET(home, out);
+  return count >= 2;
+}
+
+// The CPU the process's main thread last ran on (/proc/self/task/<pid>/stat field 39), or -1.
+int main_thread_cpu() {
+  char path[64];
+  std::snprintf(path, sizeof(path), "/proc/self/task/%d/stat", (int)getpid());
+  FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  char buf[1024] = {0};
+  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[n] = 0;
+  const char* p = std::strrchr(buf, ')');  // the command name may hold spaces
+  if (!p) return -1;
+  int field = 2;
+  for (; *p && field < 39; ++p)
+    if (*p == ' ') ++field;
+  return *p ? std::atoi(p) : -1;
+}
+
+// Where the swap workers (and the drawing thread) run.  The swap chain of an epoch reads the
+// targets the drawing thread just wrote, so they share one L3 (EPYC 9575F, 4 x 524,288: 1.3 ms
+// in one L3 against 3-4 ms placed freely and 2.25 ms on one thread).  And that L3 is not the
+// main thread's: the main thread and the HIP runtime's threads launch the learn's ~70 kernels,
+// and busy neighbours on their CCD slowed the whole step by ~4 % (measured).  mode 1: the L3 of
+// the calling thread; mode 2 (default): an L3 other than the main thread's, if there is one.
+bool l3_domain(int mode, cpu_set_t* out) {
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  const int home = sched_getcpu();
+  if (mode == 1) return home >= 0 && l3_of(home, allowed, out) && CPU_ISSET(home, out);
+  const int mcpu = main_thread_cpu();
+  cpu_set_t mine;
+  const bool have_main = mcpu >= 0 && l3_of(mcpu, allowed, &mine);
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    if (!CPU_ISSET(c, &allowed) || (have_main && CPU_ISSET(c, &mine))) continue;
+    if (l3_of(c, allowed, out) && CPU_COUNT(out) >= 4) return true;
+  }
+  return false;
 }
 
 // Persistent swap workers: epoch c's swap chain runs while epoch c+1 is drawn, without a thread
@@ -288,7 +320,8 @@ class SwapPool {
     const char* sp = std::getenv("DPPO_PERM_SPIN_MS");
     spin_ms_ = sp ? std::atoi(sp) : 0;
     const char* pe = std::getenv("DPPO_PERM_PIN");
-    pinned_ = (pe ? std::atoi(pe) : 1) && l3_domain(&l3_);
+    const int mode = pe ? std::atoi(pe) : 2;
+    pinned_ = mode != 0 && l3_domain(mode, &l3_);
     for (int i = 0; i < nw; ++i) {
       std::thread t([this] { run(); });
       if (pinned_) pthread_setaffinity_np(t.native_handle(), sizeof(l3_), &l3_);

@@ -21,6 +21,7 @@ DPPO_ENOMEM = -4
 DPPO_ECOMM = -5
 MAX_TENSORS = 16
 TRACE_FIELDS = 5
+PERM_SLOTS = 3  # pinned permutation staging slots per handle (include/dppo.h DPPO_PERM_SLOTS)
 
 EXPORTED = [
     "dppo_version", "dppo_last_error", "dppo_param_layout", "dppo_create", "dppo_destroy",

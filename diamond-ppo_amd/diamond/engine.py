@@ -26,6 +26,7 @@ Two paths, chosen once per agent:
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import threading
@@ -281,27 +282,27 @@ def hparams(cfg, lr: float, adam_step: int, betas=(0.9, 0.999)) -> N.HParams:
 
 # ---------------------------------------------------------------------------------------------
 class _DraftWorker:
-    """One long-lived host thread that draws the next learn's permutations (a thread per learn
-    cost ~0.7 ms of start-up on the launching thread).  ctypes releases the GIL during the draw."""
+    """One long-lived host thread that runs the queued permutation drafts in order (a thread per
+    learn cost ~0.7 ms of start-up on the launching thread).  ctypes releases the GIL during the
+    draw."""
 
     def __init__(self):
         self._cv = threading.Condition()
-        self._job = None
+        self._jobs = collections.deque()
         self._thread = threading.Thread(target=self._run, name="dppo-perm-draft", daemon=True)
         self._thread.start()
 
     def submit(self, fn, done: threading.Event):
         with self._cv:
-            self._job = (fn, done)
+            self._jobs.append((fn, done))
             self._cv.notify()
 
     def _run(self):
         while True:
             with self._cv:
-                while self._job is None:
+                while not self._jobs:
                     self._cv.wait()
-                fn, done = self._job
-                self._job = None
+                fn, done = self._jobs.popleft()
             try:
                 fn()
             finally:
@@ -350,9 +351,9 @@ class NativeLearner:
             self._init_comm()
         self.last_trace = None
         # host-side seconds of learn(), reported by bench.py.  Launching thread: "perms" (waiting
-        # for the look-ahead draft, which includes its wait for a free pinned slot), "draft_start"
-        # and "enqueue" (the native learn call).  Draft thread: "draw" (the permutation draws
-        # themselves: the host's own work per learn) and "slot_wait" (device back-pressure).
+        # for the look-ahead draft), "draft_start" (queueing the next drafts, including
+        # "slot_wait": device back-pressure on a pinned slot) and "enqueue" (the native learn
+        # call).  Draft thread: "draw" (the permutation draws: the host's own work per learn).
         self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "draw": 0.0,
                              "slot_wait": 0.0, "calls": 0, "lookahead_hits": 0}
         self.lookahead = os.environ.get("DPPO_PERM_LOOKAHEAD", "1") != "0"
@@ -364,7 +365,12 @@ class NativeLearner:
         env = os.environ.get("DPPO_PERM_DEVICE")
         self.device_shuffle = (env == "1") if env in ("0", "1") else (
             cfg.num_epochs * self.perm_n >= self.PERM_DEVICE_MIN)
-        self._draft = None
+        # look-ahead drafts in flight (FIFO), each chained on its predecessor's final RNG state;
+        # DPPO_PERM_DEPTH (default 2) of them, in the handle's 3 pinned slots beside the one the
+        # current learn uploads from -- two deep, a slow draw (host jitter) is absorbed instead
+        # of stalling the next learn
+        self._drafts = collections.deque()
+        self.draft_depth = max(1, min(2, int(os.environ.get("DPPO_PERM_DEPTH", "2"))))
         self._slot = 0
         self._worker = None
 
@@ -413,48 +419,65 @@ class NativeLearner:
         out = b["act_h"].numpy()
         return out.copy() if self.continuous else out.astype(np.int64)
 
-    def _start_draft(self, key: np.ndarray, pos: int):
-        """Draw the next learn's permutations (or swap targets) on the draft worker thread.
-        The worker first waits until the pinned slot's previous upload is done (device
-        back-pressure), so the launching thread never blocks here."""
-        slot = 1 - self._slot
-        d = {"slot": slot, "key_in": key.copy(), "pos_in": pos, "ok": False,
-             "device": self.device_shuffle, "done": threading.Event()}
-
+    def _start_draft(self, key: np.ndarray | None, pos: int | None):
+        """Queue the draws of one more learn's permutations (or swap targets) on the draft worker
+        thread, starting from (key, pos) -- or, when None, from the final state of the draft
+        queued before it (the worker runs drafts in order, so it is known by then)."""
+        busy = {self._slot} | {d["slot"] for d in self._drafts}
+        slot = next(k for k in range(N.PERM_SLOTS) if k not in busy)
+        prev = self._drafts[-1] if (key is None and self._drafts) else None
+        d = {"slot": slot, "key_in": None if key is None else key.copy(), "pos_in": pos,
+             "ok": False, "device": self.device_shuffle, "done": threading.Event()}
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
 
+        # The slot's previous upload must be done before the draws overwrite it: waited for here,
+        # on the launching thread (device back-pressure), not on the draft thread -- a HIP wait
+        # there slowed this thread's kernel enqueues ~2x (0.27 -> 0.55 ms per learn at C2).
+        t0 = time.perf_counter()
+        buf = d["buf"] = self.handle.perm_buffer(slot)
+        self.host_seconds["slot_wait"] += time.perf_counter() - t0
+
         def work():
-            t0 = time.perf_counter()
-            d["buf"] = buf = self.handle.perm_buffer(slot)
+            if prev is not None:
+                if not prev["ok"]:
+                    return
+                d["key_in"], d["pos_in"] = prev["key_out"].copy(), prev["pos_out"]
             t1 = time.perf_counter()
             k = d["key_in"].copy()
             d["pos_out"] = draw(k, d["pos_in"], self.perm_n, self.cfg.num_epochs, buf)
             d["key_out"] = k
-            d["t_slot"], d["t_draw"] = t1 - t0, time.perf_counter() - t1
+            d["t_draw"] = time.perf_counter() - t1
             d["ok"] = True
 
         if self._worker is None:
             self._worker = _DraftWorker()
         self._worker.submit(work, d["done"])
-        self._draft = d
+        self._drafts.append(d)
+
+    def _drain_drafts(self):
+        """Wait for every queued draft (their slots are being written) and drop them."""
+        while self._drafts:
+            self._drafts.popleft()["done"].wait()
 
     def _targets(self):
         """This learn's permutations (or, with device_shuffle, their swap targets) in a pinned
         slot; advances the global NumPy RNG exactly as num_epochs calls of
         np.random.permutation(B) would (ppo.py:254)."""
         key, pos, st = N.mt_state()
-        d, self._draft = self._draft, None
-        if d is not None:
+        if self._drafts:
+            d = self._drafts.popleft()
             d["done"].wait()
             if d["ok"]:
                 self.host_seconds["draw"] += d["t_draw"]
-                self.host_seconds["slot_wait"] += d["t_slot"]
             if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos
                     and np.array_equal(d["key_in"], key)):
                 self._slot = d["slot"]
                 N.set_mt_state(st, d["key_out"], d["pos_out"])
                 self.host_seconds["lookahead_hits"] += 1
                 return d["buf"], d["key_out"], d["pos_out"]
+            # the RNG moved between learns (or a draft failed): every later draft is chained
+            # on the wrong state
+            self._drain_drafts()
         buf = self.handle.perm_buffer(self._slot)
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
         t0 = time.perf_counter()
@@ -477,9 +500,12 @@ class NativeLearner:
             stream = torch.cuda.current_stream(self.device).cuda_stream
             pinned, key, pos = self._targets()
             t1 = time.perf_counter()
-            # the next learn's draws overlap this learn's enqueue and device time
+            # the next learns' draws overlap this learn's enqueue and device time
             if self.lookahead:
-                self._start_draft(key, pos)
+                if not self._drafts:
+                    self._start_draft(key, pos)
+                while len(self._drafts) < self.draft_depth:
+                    self._start_draft(None, None)
             t2 = time.perf_counter()
             hp = hparams(cfg, lr, step0)
             fn = (self.handle.lib.dppo_learn_targets_f32 if self.device_shuffle
