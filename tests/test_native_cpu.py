@@ -93,6 +93,42 @@ def test_host_permutations_bit_exact_with_numpy(n):
     assert np.array_equal(after[1], ref_after[1]) and after[2] == ref_after[2]
 
 
+_POOL_SCRIPT = r"""
+import sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from diamond import _native as N
+n, count = 1 << 17, 4
+res = {}
+def draft():  # from a non-main thread, as the learn() look-ahead calls it
+    out = np.empty(count * n, np.int32)
+    for seed in (5, 6):
+        np.random.seed(seed)
+        key, pos, _ = N.mt_state()
+        pos = N.perm_numpy(key, pos, n, count, out)
+        np.random.seed(seed)
+        ref = np.concatenate([np.random.permutation(n) for _ in range(count)])
+        st = np.random.get_state()
+        res[seed] = bool(np.array_equal(out, ref) and np.array_equal(key, st[1]) and pos == st[2])
+t = threading.Thread(target=draft)
+t.start()
+t.join()
+print("OK" if res and all(res.values()) else "MISMATCH", res)
+"""
+
+
+def test_host_permutations_swap_pool_bit_exact():
+    """The pooled path (each epoch's swap chain on a persistent worker while the next epoch is
+    drawn; DPPO_PERM_PIN=1 puts the pool in the caller's L3, so it runs in this container too)
+    reproduces np.random.permutation exactly, epochs in order, RNG state included."""
+    import subprocess
+    import sys
+    env = dict(os.environ, DPPO_PERM_PIN="1", DPPO_PERM_WORKERS="3")
+    r = subprocess.run([sys.executable, "-c", _POOL_SCRIPT, os.path.join(ROOT, "diamond-ppo_amd")],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, (1 << 16) + 3])
 def test_host_swap_targets_replay_to_numpy_permutation(n):
     """dppo_perm_targets_numpy = the MT19937 half of np.random.permutation: replaying its
