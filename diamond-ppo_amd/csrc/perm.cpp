@@ -392,35 +392,91 @@ extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, i
   return DPPO_OK;
 }
 
-extern "C" int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
-                               int32_t* out) {
-  if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
+namespace {
+
+// An in-flight permutation draw: the swaps still running on the pool and the target scratch they
+// read.  Scratch buffers are recycled (a fresh 8 MiB buffer per call costs ~2,000 first-touch page
+// faults), at most a few at a time: one per draft in flight.
+struct PermTicket {
+  SwapPool::Batch batch;
+  std::vector<int32_t> scratch;
+  bool pooled = false;
+};
+std::mutex g_scratch_mu;
+std::vector<std::vector<int32_t>> g_scratch_free;
+
+std::vector<int32_t> take_scratch(size_t n) {
+  std::lock_guard<std::mutex> g(g_scratch_mu);
+  for (size_t i = 0; i < g_scratch_free.size(); ++i)
+    if (g_scratch_free[i].size() >= n) {
+      std::vector<int32_t> v = std::move(g_scratch_free[i]);
+      g_scratch_free.erase(g_scratch_free.begin() + (long)i);
+      return v;
+    }
+  return std::vector<int32_t>(n);
+}
+void give_scratch(std::vector<int32_t>&& v) {
+  std::lock_guard<std::mutex> g(g_scratch_mu);
+  if (g_scratch_free.size() < 4) g_scratch_free.push_back(std::move(v));
+}
+
+// Targets first (into the ticket's scratch), then the swaps into out -- the same state machine as
+// numpy's fused loop.  The draws are one sequential MT19937 stream; the swaps of epoch c only need
+// epoch c's targets, so at minibatch sizes they run on the pool while the next epoch is drawn,
+// and the caller may start the NEXT draw (from the returned RNG state) before they finish.
+int perm_start(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out,
+               PermTicket* t) {
   MT g;
   g.load(key, *pos);
-  // Targets first (into a per-thread scratch that persists across calls), then the swaps into
-  // out -- the same state machine as numpy's fused loop.  The draws are one sequential MT19937
-  // stream; the swaps of epoch c only need epoch c's targets, so at minibatch sizes they run on
-  // the pool while the next epoch is drawn (wall ~ draws + one epoch's swaps).
-  static thread_local std::vector<int32_t> scratch;
-  if (scratch.size() < (size_t)(n * count)) scratch.resize((size_t)(n * count));
   static const int pool_mode = [] {
     const char* e = std::getenv("DPPO_PERM_POOL");
     return e ? std::atoi(e) : 1;
   }();
   // unpinned workers lose to one thread (see l3_domain): pool only inside one L3 domain
-  const bool pooled = pool_mode && n >= (1 << 16) && count > 1 && SwapPool::get().pinned();
-  SwapPool::Batch batch;
-  if (pooled) SwapPool::get().pin_caller();
+  t->pooled = pool_mode && n >= (1 << 16) && count > 1 && SwapPool::get().pinned();
+  t->scratch = take_scratch((size_t)(n * count));
+  if (t->pooled) SwapPool::get().pin_caller();
   for (int32_t c = 0; c < count; ++c) {
-    int32_t* j = scratch.data() + (int64_t)c * n;
+    int32_t* j = t->scratch.data() + (int64_t)c * n;
     draw_targets(g, n, 1, j);
-    if (pooled)
-      SwapPool::get().submit(&batch, out + (int64_t)c * n, j, n);
+    if (t->pooled)
+      SwapPool::get().submit(&t->batch, out + (int64_t)c * n, j, n);
     else
       apply_swaps(out + (int64_t)c * n, j, n);
   }
-  if (pooled) SwapPool::wait(&batch);
   std::memcpy(key, g.mt, sizeof(g.mt));
   *pos = g.pos;
+  return DPPO_OK;
+}
+
+void perm_finish(PermTicket* t) {
+  if (t->pooled) SwapPool::wait(&t->batch);
+  give_scratch(std::move(t->scratch));
+  delete t;
+}
+
+}  // namespace
+
+extern "C" int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
+                               int32_t* out) {
+  if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
+  PermTicket* t = new PermTicket();
+  const int rc = perm_start(key, pos, n, count, out, t);
+  perm_finish(t);
+  return rc;
+}
+
+extern "C" int dppo_perm_numpy_async(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
+                                     int32_t* out, void** ticket) {
+  if (!ticket || bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
+  PermTicket* t = new PermTicket();
+  const int rc = perm_start(key, pos, n, count, out, t);
+  *ticket = t;
+  return rc;
+}
+
+extern "C" int dppo_perm_wait(void* ticket) {
+  if (!ticket) return DPPO_EINVAL;
+  perm_finish(static_cast<PermTicket*>(ticket));
   return DPPO_OK;
 }

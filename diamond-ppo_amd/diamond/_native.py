@@ -29,7 +29,7 @@ EXPORTED = [
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_resolve", "dppo_act_f32", "dppo_loopback_group",
+    "dppo_perm_targets_numpy", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_resolve", "dppo_act_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
@@ -110,6 +110,8 @@ def load():
         "dppo_get_trace": (ctypes.c_int, [vp, vp, i32]),
         "dppo_perm_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
         "dppo_perm_targets_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
+        "dppo_perm_numpy_async": (ctypes.c_int, [vp, P(i32), i64, i32, vp, P(vp)]),
+        "dppo_perm_wait": (ctypes.c_int, [vp]),
         "dppo_perm_resolve": (ctypes.c_int, [vp, vp, i64, i32, vp, vp]),
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
@@ -176,6 +178,21 @@ def perm_numpy(key: np.ndarray, pos: int, n: int, count: int, out: np.ndarray | 
     """NumPy-legacy-exact permutations (host C++).  ``key`` (uint32[624]) is advanced in place;
     returns the new ``pos``.  ``out`` is an int32 array of count*n or a raw host address."""
     return _mt_call("dppo_perm_numpy", key, pos, n, count, out)
+
+
+def perm_numpy_async(key: np.ndarray, pos: int, n: int, count: int, out: int):
+    """:func:`perm_numpy` whose swaps may still be running on the host pool when it returns:
+    (new pos, ticket); ``perm_wait(ticket)`` before ``out`` is read."""
+    assert key.dtype == np.uint32 and key.size == 624 and key.flags.c_contiguous
+    p = ctypes.c_int32(int(pos))
+    t = ctypes.c_void_p()
+    check(load().dppo_perm_numpy_async(key.ctypes.data, ctypes.byref(p), int(n), int(count),
+                                       out, ctypes.byref(t)), "dppo_perm_numpy_async")
+    return int(p.value), t.value
+
+
+def perm_wait(ticket) -> None:
+    check(load().dppo_perm_wait(ticket), "dppo_perm_wait")
 
 
 def perm_targets_numpy(key: np.ndarray, pos: int, n: int, count: int,

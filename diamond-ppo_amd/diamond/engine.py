@@ -444,7 +444,13 @@ class NativeLearner:
                 d["key_in"], d["pos_in"] = prev["key_out"].copy(), prev["pos_out"]
             t1 = time.perf_counter()
             k = d["key_in"].copy()
-            d["pos_out"] = draw(k, d["pos_in"], self.perm_n, self.cfg.num_epochs, buf)
+            if self.device_shuffle:
+                d["pos_out"] = draw(k, d["pos_in"], self.perm_n, self.cfg.num_epochs, buf)
+            else:
+                # returns after the draws: the last epochs' swaps finish on the host pool while
+                # the next draft's draws (chained on key_out) already run
+                d["pos_out"], d["ticket"] = N.perm_numpy_async(k, d["pos_in"], self.perm_n,
+                                                               self.cfg.num_epochs, buf)
             d["key_out"] = k
             d["t_draw"] = time.perf_counter() - t1
             d["ok"] = True
@@ -454,10 +460,18 @@ class NativeLearner:
         self._worker.submit(work, d["done"])
         self._drafts.append(d)
 
+    @staticmethod
+    def _finish(d):
+        """Wait for a draft's draws and for the swaps still running on the host pool."""
+        d["done"].wait()
+        t = d.pop("ticket", None)
+        if t is not None:
+            N.perm_wait(t)
+
     def _drain_drafts(self):
         """Wait for every queued draft (their slots are being written) and drop them."""
         while self._drafts:
-            self._drafts.popleft()["done"].wait()
+            self._finish(self._drafts.popleft())
 
     def _targets(self):
         """This learn's permutations (or, with device_shuffle, their swap targets) in a pinned
@@ -466,7 +480,7 @@ class NativeLearner:
         key, pos, st = N.mt_state()
         if self._drafts:
             d = self._drafts.popleft()
-            d["done"].wait()
+            self._finish(d)
             if d["ok"]:
                 self.host_seconds["draw"] += d["t_draw"]
             if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos

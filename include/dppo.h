@@ -226,6 +226,14 @@ int dppo_get_trace(dppo_handle* h, float* host_out, int32_t rows);
  * np.random.permutation would.  Host only. */
 int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
 
+/* dppo_perm_numpy in two halves: returns once the draws are done (key / pos already advanced, so
+ * the next learn's draws may start) while the Fisher-Yates swaps finish on the host worker pool;
+ * dppo_perm_wait(ticket) waits for them (out is complete afterwards) and frees the ticket.  Every
+ * ticket must be waited for exactly once.  Host only. */
+int dppo_perm_numpy_async(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out,
+                          void** ticket);
+int dppo_perm_wait(void* ticket);
+
 /* The MT19937 half of dppo_perm_numpy: the Fisher-Yates swap targets out[c][i] = j_i
  * (i = n-1 .. 1; out[c][0] = 0) of `count` successive permutations, advancing key/pos exactly
  * as dppo_perm_numpy does.  Host only. */
