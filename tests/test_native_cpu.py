@@ -110,17 +110,32 @@ def draft():  # from a non-main thread, as the learn() look-ahead calls it
         ref = np.concatenate([np.random.permutation(n) for _ in range(count)])
         st = np.random.get_state()
         res[seed] = bool(np.array_equal(out, ref) and np.array_equal(key, st[1]) and pos == st[2])
-t = threading.Thread(target=draft)
-t.start()
-t.join()
-print("OK" if res and all(res.values()) else "MISMATCH", res)
+def chained():  # two async drafts in a row, the second from the first's returned state
+    bufs = [np.empty(count * n, np.int32) for _ in range(2)]
+    np.random.seed(9)
+    key, pos, _ = N.mt_state()
+    pos1, t1 = N.perm_numpy_async(key, pos, n, count, bufs[0].ctypes.data)
+    pos2, t2 = N.perm_numpy_async(key, pos1, n, count, bufs[1].ctypes.data)
+    N.perm_wait(t1)
+    N.perm_wait(t2)
+    np.random.seed(9)
+    ref = [np.concatenate([np.random.permutation(n) for _ in range(count)]) for _ in range(2)]
+    st = np.random.get_state()
+    res["async"] = bool(np.array_equal(bufs[0], ref[0]) and np.array_equal(bufs[1], ref[1])
+                        and np.array_equal(key, st[1]) and pos2 == st[2])
+for fn in (draft, chained):
+    t = threading.Thread(target=fn)
+    t.start()
+    t.join()
+print("OK" if len(res) == 3 and all(res.values()) else "MISMATCH", res)
 """
 
 
 def test_host_permutations_swap_pool_bit_exact():
     """The pooled path (each epoch's swap chain on a persistent worker while the next epoch is
     drawn; DPPO_PERM_PIN=1 puts the pool in the caller's L3, so it runs in this container too)
-    reproduces np.random.permutation exactly, epochs in order, RNG state included."""
+    reproduces np.random.permutation exactly, epochs in order, RNG state included -- also as two
+    chained dppo_perm_numpy_async drafts whose swaps are waited for afterwards."""
     import subprocess
     import sys
     env = dict(os.environ, DPPO_PERM_PIN="1", DPPO_PERM_WORKERS="3")
