@@ -255,9 +255,9 @@ int main_thread_cpu() {
 // Where the swap workers (and the drawing thread) run.  The swap chain of an epoch reads the
 // targets the drawing thread just wrote, so they share one L3 (EPYC 9575F, 4 x 524,288: 1.3 ms
 // in one L3 against 3-4 ms placed freely and 2.25 ms on one thread).  And that L3 is not the
-// main thread's: the main thread and the HIP runtime's threads launch the learn's ~70 kernels,
-// and busy neighbours on their CCD slowed the whole step by ~4 % (measured).  mode 1: the L3 of
-// the calling thread; mode 2 (default): an L3 other than the main thread's, if there is one.
+// main thread's where the process may use another: the main thread and the HIP runtime's threads
+// launch the learn's ~70 kernels.  mode 1: the L3 of the calling thread; mode 2 (default): an L3
+// other than the main thread's, else the caller's.
 bool l3_domain(int mode, cpu_set_t* out) {
   cpu_set_t allowed;
   if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
@@ -270,7 +270,10 @@ bool l3_domain(int mode, cpu_set_t* out) {
     if (!CPU_ISSET(c, &allowed) || (have_main && CPU_ISSET(c, &mine))) continue;
     if (l3_of(c, allowed, out) && CPU_COUNT(out) >= 4) return true;
   }
-  return false;
+  // every allowed CPU shares the main thread's L3 (a cpuset of one CCD): the caller's L3 still
+  // beats an unpinned pool or one thread (measured equal to mode 2 once the slot waits moved off
+  // the draft thread)
+  return home >= 0 && l3_of(home, allowed, out) && CPU_ISSET(home, out);
 }
 
 // Persistent swap workers: epoch c's swap chain runs while epoch c+1 is drawn, without a thread
