@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -74,7 +75,7 @@ __attribute__((target_clones("avx512f", "avx2", "default"))) void twist_block(ui
 
 struct MT {
   uint32_t mt[kN];
-  uint32_t out[kN];  // tempered outputs of the current block
+  uint32_t out[kN];  // tempered outputs of the current block (when twisted in this thread)
   int pos;           // next unconsumed word of the block (numpy's `pos`)
 
   void load(const uint32_t* key, int p) {
@@ -143,8 +144,21 @@ bool has_avx512() {
 // accept step branch-free (the draw is always stored; i only advances on acceptance).
 // Within one mask band [lo, i] the loop runs min(words left in the block, i - lo + 1) draws
 // with no exit test: i falls by at most one per draw, so it cannot leave the band early.
-void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
-  int opos = g.pos;
+// The MT19937 blocks the draws consume: twisted here (LocalBlocks) or by a producer thread
+// running ahead (RingBlocks).  next() returns the next block's 624 tempered words.
+struct LocalBlocks {
+  MT& g;
+  const uint32_t* first() const { return g.out; }
+  const uint32_t* next() {
+    twist_block(g.mt, g.out);
+    return g.out;
+  }
+};
+
+template <class Blocks>
+const uint32_t* draw_targets_from(Blocks& src, const uint32_t* blk, int& pos, int64_t n,
+                                  int32_t count, int32_t* __restrict out) {
+  int opos = pos;
   const bool simd = has_avx512();
   for (int32_t c = 0; c < count; ++c) {
     int32_t* __restrict j = out + (int64_t)c * n;
@@ -155,14 +169,14 @@ void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
       const uint32_t lo = (mask >> 1) + 1;  // all draws in [lo, i] share this mask
       while (i >= lo) {
         if (opos >= kN) {
-          twist_block(g.mt, g.out);
+          blk = src.next();
           opos = 0;
         }
         if (simd && i >= lo + 15) {
-          opos += (int)draw_groups_avx512(g.out + opos, (uint32_t)(kN - opos), mask, i, lo, j);
+          opos += (int)draw_groups_avx512(blk + opos, (uint32_t)(kN - opos), mask, i, lo, j);
           if (opos >= kN || i < lo) continue;
         }
-        const uint32_t* __restrict o = g.out + opos;
+        const uint32_t* __restrict o = blk + opos;
         const uint32_t left = (uint32_t)(kN - opos);
         uint32_t run = left < i - lo + 1 ? left : i - lo + 1;
         if (simd && run > 16) run = 16;  // one group by the serial chain, then SIMD again
@@ -181,8 +195,69 @@ void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
       }
     }
   }
-  g.pos = opos;
+  pos = opos;
+  return blk;
 }
+
+void draw_targets(MT& g, int64_t n, int32_t count, int32_t* __restrict out) {
+  LocalBlocks src{g};
+  draw_targets_from(src, src.first(), g.pos, n, count, out);
+}
+
+// numpy's state key is the untempered block: tempering is a bijection, so the key of a block
+// that was twisted in another thread is recovered from its tempered words.
+inline uint32_t untemper(uint32_t y) {
+  y ^= y >> 18;
+  y ^= (y << 15) & 0xEFC60000u;
+  uint32_t x = y;
+  for (int k = 0; k < 4; ++k) x = y ^ ((x << 7) & 0x9D2C5680u);
+  y = x;
+  return y ^ (y >> 11) ^ (y >> 22);
+}
+
+// A producer thread twists the blocks ahead of the drawing thread into a single-producer /
+// single-consumer ring (the twist is ~37 % of the draw time): the draws then cost the accept
+// scan alone.  A slot is released when the consumer moves past it.
+class RingBlocks {
+ public:
+  explicit RingBlocks(const uint32_t* key, const cpu_set_t* cpus) {
+    std::memcpy(mt_, key, sizeof(mt_));
+    th_ = std::thread([this] { produce(); });
+    if (cpus) pthread_setaffinity_np(th_.native_handle(), sizeof(*cpus), cpus);
+  }
+  ~RingBlocks() {
+    stop_.store(true, std::memory_order_relaxed);
+    th_.join();
+  }
+  const uint32_t* next() {
+    if (held_) tail_.store(tail_.load(std::memory_order_relaxed) + 1, std::memory_order_release);
+    held_ = true;
+    const uint64_t t = tail_.load(std::memory_order_relaxed);
+    while (head_.load(std::memory_order_acquire) == t) _mm_pause();
+    return slots_[t % kCap];
+  }
+
+ private:
+  static constexpr int kCap = 32;
+  void produce() {
+    uint64_t h = 0;
+    while (!stop_.load(std::memory_order_relaxed)) {
+      if (h - tail_.load(std::memory_order_acquire) >= (uint64_t)kCap) {
+        _mm_pause();
+        continue;
+      }
+      twist_block(mt_, slots_[h % kCap]);
+      head_.store(++h, std::memory_order_release);
+    }
+  }
+  alignas(64) uint32_t slots_[kCap][kN];
+  uint32_t mt_[kN];
+  alignas(64) std::atomic<uint64_t> head_{0};
+  alignas(64) std::atomic<uint64_t> tail_{0};
+  std::atomic<bool> stop_{false};
+  bool held_ = false;
+  std::thread th_;
+};
 
 // a[0..n) = arange(n) shuffled by the Fisher-Yates targets j: the sequential swap loop for
 // i = n-1 .. 1, with the target lines prefetched ahead.
@@ -336,6 +411,7 @@ class SwapPool {
   // A draft thread (not the main thread: its affinity would be inherited by every thread it
   // starts later) joins the workers' L3 domain, once.
   bool pinned() const { return pinned_; }
+  const cpu_set_t* cpus() const { return pinned_ ? &l3_ : nullptr; }
   void pin_caller() {
     static thread_local bool done = false;
     if (done || !pinned_) return;
@@ -439,16 +515,31 @@ int perm_start(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* o
   t->pooled = pool_mode && n >= (1 << 16) && count > 1 && SwapPool::get().pinned();
   t->scratch = take_scratch((size_t)(n * count));
   if (t->pooled) SwapPool::get().pin_caller();
+  // beside the pool, a producer thread twists the MT19937 blocks ahead of the draws
+  static const int ring_mode = [] {
+    const char* e = std::getenv("DPPO_PERM_RING");
+    return e ? std::atoi(e) : 1;
+  }();
+  std::unique_ptr<RingBlocks> ring;
+  if (t->pooled && ring_mode && n * count >= (1 << 20))
+    ring.reset(new RingBlocks(g.mt, SwapPool::get().cpus()));
+  LocalBlocks local{g};
+  const uint32_t* blk = g.out;
+  int p = g.pos;
   for (int32_t c = 0; c < count; ++c) {
     int32_t* j = t->scratch.data() + (int64_t)c * n;
-    draw_targets(g, n, 1, j);
+    blk = ring ? draw_targets_from(*ring, blk, p, n, 1, j) : draw_targets_from(local, blk, p, n, 1, j);
     if (t->pooled)
       SwapPool::get().submit(&t->batch, out + (int64_t)c * n, j, n);
     else
       apply_swaps(out + (int64_t)c * n, j, n);
   }
-  std::memcpy(key, g.mt, sizeof(g.mt));
-  *pos = g.pos;
+  if (ring && blk != g.out) {
+    for (int k = 0; k < kN; ++k) key[k] = untemper(blk[k]);
+  } else {
+    std::memcpy(key, g.mt, sizeof(g.mt));
+  }
+  *pos = p;
   return DPPO_OK;
 }
 
