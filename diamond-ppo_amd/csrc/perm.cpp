@@ -341,9 +341,25 @@ bool l3_domain(int mode, cpu_set_t* out) {
   const int mcpu = main_thread_cpu();
   cpu_set_t mine;
   const bool have_main = mcpu >= 0 && l3_of(mcpu, allowed, &mine);
+  // the candidate L3 domains (>= 4 allowed CPUs, not the main thread's), in CPU order
+  std::vector<cpu_set_t> doms;
+  cpu_set_t seen;
+  CPU_ZERO(&seen);
   for (int c = 0; c < CPU_SETSIZE; ++c) {
-    if (!CPU_ISSET(c, &allowed) || (have_main && CPU_ISSET(c, &mine))) continue;
-    if (l3_of(c, allowed, out) && CPU_COUNT(out) >= 4) return true;
+    if (!CPU_ISSET(c, &allowed) || CPU_ISSET(c, &seen)) continue;
+    cpu_set_t d;
+    if (!l3_of(c, allowed, &d)) continue;
+    CPU_OR(&seen, &seen, &d);
+    if ((have_main && CPU_ISSET(c, &mine)) || CPU_COUNT(&d) < 4) continue;
+    doms.push_back(d);
+  }
+  if (!doms.empty()) {
+    // one process per GPU (torchrun's LOCAL_RANK): spread the ranks' pools over the domains
+    // instead of stacking every rank's draft and swap threads on the first one
+    const char* lr = std::getenv("LOCAL_RANK");
+    const size_t k = lr ? (size_t)std::max(0, std::atoi(lr)) % doms.size() : 0;
+    *out = doms[k];
+    return true;
   }
   // every allowed CPU shares the main thread's L3 (a cpuset of one CCD): the caller's L3 still
   // beats an unpinned pool or one thread (measured equal to mode 2 once the slot waits moved off
