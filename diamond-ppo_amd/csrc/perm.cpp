@@ -502,17 +502,30 @@ std::vector<std::vector<int32_t>> g_scratch_free;
 
 std::vector<int32_t> take_scratch(size_t n) {
   std::lock_guard<std::mutex> g(g_scratch_mu);
+  size_t best = g_scratch_free.size();  // the smallest buffer that fits
   for (size_t i = 0; i < g_scratch_free.size(); ++i)
-    if (g_scratch_free[i].size() >= n) {
-      std::vector<int32_t> v = std::move(g_scratch_free[i]);
-      g_scratch_free.erase(g_scratch_free.begin() + (long)i);
-      return v;
-    }
+    if (g_scratch_free[i].size() >= n &&
+        (best == g_scratch_free.size() || g_scratch_free[i].size() < g_scratch_free[best].size()))
+      best = i;
+  if (best < g_scratch_free.size()) {
+    std::vector<int32_t> v = std::move(g_scratch_free[best]);
+    g_scratch_free.erase(g_scratch_free.begin() + (long)best);
+    return v;
+  }
   return std::vector<int32_t>(n);
 }
 void give_scratch(std::vector<int32_t>&& v) {
   std::lock_guard<std::mutex> g(g_scratch_mu);
-  if (g_scratch_free.size() < 4) g_scratch_free.push_back(std::move(v));
+  if (g_scratch_free.size() < 4) {
+    g_scratch_free.push_back(std::move(v));
+    return;
+  }
+  // full: a larger buffer replaces the smallest (a handle with a larger batch after a smaller
+  // one otherwise allocated -- and zero-filled -- a fresh buffer on every call)
+  size_t k = 0;
+  for (size_t i = 1; i < g_scratch_free.size(); ++i)
+    if (g_scratch_free[i].size() < g_scratch_free[k].size()) k = i;
+  if (g_scratch_free[k].size() < v.size()) g_scratch_free[k] = std::move(v);
 }
 
 // Targets first (into the ticket's scratch), then the swaps into out -- the same state machine as
