@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "common.h"
+#include "loop_sync.h"
 
 namespace dppo {
 
@@ -63,15 +64,7 @@ struct dppo_handle;
 // "done", host barrier, wait for every peer's "done" (nobody still reads this rank's buffer), copy
 // the sum back.  RCCL refuses two ranks on one GPU; this is how the N > 1 data path
 // (statistics / gradient exchange, global divisors, rank-0-only terms) is parity-tested on one.
-struct LoopGroup {
-  int n = 0;
-  std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t gen = 0;
-  // set when a barrier timed out or a member was destroyed: every member's exchange then fails
-  // with DPPO_ECOMM (arrival counts and peer buffers can no longer be trusted)
-  bool broken = false;
+struct LoopGroup : LoopSync {
   dppo_handle* members[kMaxLoopRanks] = {};
   void* bufs[kMaxLoopRanks] = {};
 };
@@ -329,35 +322,25 @@ int require_mlp(const dppo_handle* h) {
   return DPPO_OK;
 }
 
-// ranks taking part in the exchanges (RCCL communicator or loopback group), else 1
-inline bool distributed(const dppo_handle* h) { return (h->comm || h->loop) && h->nranks > 1; }
+// Whether learn() takes the exchanging (multi-rank) sequence: an RCCL communicator of any size
+// -- a 1-rank one too, so the collective path (slab reduce -> ncclAllReduce -> clip + Adam, the
+// advantage-stat all-reduce) runs and is tested on a single GPU -- or a loopback group.
+inline bool distributed(const dppo_handle* h) {
+  return h->comm != nullptr || (h->loop && h->nranks > 1);
+}
 inline int world_of(const dppo_handle* h) { return distributed(h) ? h->nranks : 1; }
 
 int loop_barrier(LoopGroup* g) {
-  std::unique_lock<std::mutex> lk(g->mu);
-  if (g->broken) {
-    set_error("loopback group is broken (an earlier exchange timed out or a member was destroyed)");
-    return DPPO_ECOMM;
+  switch (g->barrier(std::chrono::seconds(120))) {
+    case LoopSync::kOk:
+      return DPPO_OK;
+    case LoopSync::kTimeout:
+      set_error("loopback group: a rank did not reach the all-reduce within 120 s");
+      return DPPO_ECOMM;
+    default:
+      set_error("loopback group is broken (an exchange timed out or a member was destroyed)");
+      return DPPO_ECOMM;
   }
-  const uint64_t gen = g->gen;
-  if (++g->arrived == g->n) {
-    g->arrived = 0;
-    ++g->gen;
-    g->cv.notify_all();
-    return DPPO_OK;
-  }
-  if (!g->cv.wait_for(lk, std::chrono::seconds(120),
-                      [&] { return g->gen != gen || g->broken; })) {
-    g->broken = true;
-    g->cv.notify_all();
-    set_error("loopback group: a rank did not reach the all-reduce within 120 s");
-    return DPPO_ECOMM;
-  }
-  if (g->gen == gen) {  // woken by a break, not by the last arriver
-    set_error("loopback group is broken (an exchange timed out or a member was destroyed)");
-    return DPPO_ECOMM;
-  }
-  return DPPO_OK;
 }
 
 int loop_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s) {
@@ -372,18 +355,36 @@ int loop_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s)
   // wait on another rank's stream: with more ranks than hardware queues (GPU_MAX_HW_QUEUES)
   // streams share queues, and a cross-stream barrier packet could then wait on work queued behind
   // it.  Test-only path: two host synchronisations per exchange are fine.
-  g->bufs[h->rank] = buf;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->bufs[h->rank] = buf;
+  }
   DPPO_HIP_CHECK(hipEventRecord(h->loop_ready, s));
   DPPO_TRY(loop_barrier(g));
+  // The peers' buffers and events are read, and their events waited for, under the group lock:
+  // a peer being destroyed (dppo_destroy takes the lock to clear its slot and break the group
+  // before it frees anything) then fails the exchange instead of being read after it is freed.
+  // Waiting under the lock cannot deadlock: every awaited event was recorded before its rank
+  // entered the barrier just passed, so it completes without any host progress.
   RankPtrs src{};
-  for (int r = 0; r < g->n; ++r) {
-    src.p[r] = g->bufs[r];
-    DPPO_HIP_CHECK(hipEventSynchronize(g->members[r]->loop_ready));
-  }
+  auto wait_peers = [&](bool done) -> int {
+    std::lock_guard<std::mutex> lk(g->mu);
+    for (int r = 0; r < g->n; ++r) {
+      if (g->broken || !g->members[r] || !g->bufs[r]) {
+        set_error("loopback group is broken (a member was destroyed during an exchange)");
+        return DPPO_ECOMM;
+      }
+      src.p[r] = g->bufs[r];
+      DPPO_HIP_CHECK(
+          hipEventSynchronize(done ? g->members[r]->loop_done : g->members[r]->loop_ready));
+    }
+    return DPPO_OK;
+  };
+  DPPO_TRY(wait_peers(false));
   DPPO_TRY(launch_rank_sum(src, g->n, h->loop_out, (int64_t)n, f64, s));
   DPPO_HIP_CHECK(hipEventRecord(h->loop_done, s));
   DPPO_TRY(loop_barrier(g));
-  for (int r = 0; r < g->n; ++r) DPPO_HIP_CHECK(hipEventSynchronize(g->members[r]->loop_done));
+  DPPO_TRY(wait_peers(true));
   DPPO_HIP_CHECK(hipMemcpyAsync(buf, h->loop_out, bytes, hipMemcpyDeviceToDevice, s));
   return DPPO_OK;
 }
@@ -839,10 +840,9 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipDeviceSynchronize();
   if (h->loop) {  // peers must never touch this handle's events or buffers again
     std::lock_guard<std::mutex> lk(h->loop->mu);
-    h->loop->broken = true;
     h->loop->members[h->rank] = nullptr;
     h->loop->bufs[h->rank] = nullptr;
-    h->loop->cv.notify_all();
+    h->loop->break_locked();
   }
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->loop_out) (void)hipFree(h->loop_out);
@@ -910,6 +910,26 @@ int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream) {
   return launch_stats_finalize(h->dsum, n, mean_std, S(stream));
 }
 
+int dppo_adv_sums(dppo_handle* h, double* sums, void* stream) {
+  if (!h || !sums) {
+    set_error("null argument to dppo_adv_sums");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, S(stream)));
+  DPPO_HIP_CHECK(hipMemcpyAsync(sums, h->dsum, 2 * sizeof(double), hipMemcpyDeviceToDevice,
+                                S(stream)));
+  return DPPO_OK;
+}
+
+int dppo_adv_stats_from_sums(const double* sums, double n_total, float* mean_std, void* stream) {
+  if (!sums || !mean_std || !(n_total >= 1.0)) {
+    set_error("invalid argument to dppo_adv_stats_from_sums");
+    return DPPO_EINVAL;
+  }
+  return launch_stats_finalize(sums, n_total, mean_std, S(stream));
+}
+
 int dppo_adv_normalize_f32(float* adv, const float* mean_std, int64_t n, void* stream) {
   if (!adv || !mean_std || n < 0) {
     set_error("invalid argument to dppo_adv_normalize_f32");
@@ -942,6 +962,31 @@ int dppo_act_f32(dppo_handle* h, const float* params, const float* obs, int64_t 
   DPPO_TRY(require_mlp(h));
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   return launch_act(h->sh, h->po, params, obs, actions, n, seed, counter, S(stream));
+}
+
+int dppo_act_squash_f32(dppo_handle* h, const float* params, const float* obs, int64_t n,
+                        uint64_t seed, uint64_t counter, const float* low, const float* high,
+                        float* actions, float* env_actions, void* stream) {
+  if (!h || !params || !obs || !actions || !env_actions || n < 0 || (!low) != (!high)) {
+    set_error("invalid argument to dppo_act_squash_f32");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(require_mlp(h));
+  if (!h->dims.continuous) {
+    set_error("dppo_act_squash_f32 needs a continuous (Box) action space");
+    return DPPO_EINVAL;
+  }
+  if (low) {
+    for (int j = 0; j < h->dims.act_dim; ++j) {
+      if (!std::isfinite(low[j]) || !std::isfinite(high[j]) || !(high[j] > low[j])) {
+        set_error("dppo_act_squash_f32: bounds must be finite with high > low (dim %d)", j);
+        return DPPO_EINVAL;
+      }
+    }
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  const ActSquash sq{env_actions, low, high};
+  return launch_act(h->sh, h->po, params, obs, actions, n, seed, counter, S(stream), nullptr, &sq);
 }
 
 int dppo_actor_forward_f32(dppo_handle* h, const float* params, const float* obs, int64_t n,
@@ -1064,12 +1109,14 @@ int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out) {
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   if (h->perm_copy_pending[slot]) {
-    // polled with sleeps, not hipEventSynchronize: this runs on the draft thread, where a blocking
-    // (spinning) wait slowed the launching thread's kernel enqueues ~2x (0.24 -> 0.55 ms per
-    // learn) and left gaps between the learn's kernels
+    // Runs on the launching thread (engine._start_draft claims a slot before queueing its draft):
+    // the slot's previous upload was enqueued two learns earlier and is normally long done, so
+    // this is one hipEventQuery.  When it is not, it is polled with short sleeps rather than a
+    // spinning hipEventSynchronize, which competes with the HIP runtime's submission threads
+    // (measured on the draft thread: kernel enqueues 0.24 -> 0.55 ms per learn).
     hipError_t e;
     while ((e = hipEventQuery(h->perm_copy_done[slot])) == hipErrorNotReady)
-      std::this_thread::sleep_for(std::chrono::microseconds(50));
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
     if (e != hipSuccess) {
       set_error("hipEventQuery: %s", hipGetErrorString(e));
       return DPPO_EHIP;

@@ -191,9 +191,16 @@ size_t mlp_lds_bytes_eval(const MlpShape& sh);
 int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                 const void* actions, const float* next_obs, float* logp, float* values,
                 float* next_values, int64_t n, hipStream_t s);
+// optional env-action output of the continuous act kernel: tanh(u), rescaled to [low, high]
+// when both bound arrays are given (host arrays of A floats)
+struct ActSquash {
+  float* env_actions;
+  const float* low;
+  const float* high;
+};
 int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s,
-               float* heads = nullptr);
+               float* heads = nullptr, const ActSquash* squash = nullptr);
 struct GradArgs {
   const float* params;
   const float* rec;

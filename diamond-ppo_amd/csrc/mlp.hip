@@ -384,6 +384,11 @@ struct ActArgs {
   const float* obs;
   void* actions;   // sampled actions, or null (heads only)
   float* heads;    // optional [n][A]: the logits / Gaussian means the samples are drawn from
+  // optional [n][A] (continuous): the environment's action for each Gaussian sample u --
+  // tanh(u) (squash 1) or low + (tanh(u) + 1) * (high - low) / 2 (squash 2)
+  float* env_act;
+  int squash;
+  float sq_lo[16], sq_half[16];
   int64_t n;
   uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
   int D, D8, nq1, A;
@@ -457,8 +462,23 @@ __global__ __launch_bounds__(kThreads, 4) void act_kernel(ActArgs a) {
             float sn, cs;
             __sincosf(6.28318530717958647692f * u01(c[2 * p + 1]), &sn, &cs);
             const int k = k0 + 2 * p;
-            if (k < a.A) act[k] = out[k] + __expf(lds[L.ls + k]) * (r * cs);
-            if (k + 1 < a.A) act[k + 1] = out[k + 1] + __expf(lds[L.ls + k + 1]) * (r * sn);
+            const float u0 = k < AMAX ? out[k] + __expf(lds[L.ls + k]) * (r * cs) : 0.f;
+            const float u1 = k + 1 < AMAX ? out[k + 1] + __expf(lds[L.ls + k + 1]) * (r * sn) : 0.f;
+            if (k < a.A) act[k] = u0;
+            if (k + 1 < a.A) act[k + 1] = u1;
+            if (a.env_act) {
+              // the squashed env action (SURVEY 8 f2 extension; the reference samples the raw
+              // Gaussian, continuous_ppo.py:83-93): accurate tanhf, not the MLP's fast form
+              float* env = a.env_act + i * a.A;
+              if (k < a.A) {
+                const float t0 = tanhf(u0);
+                env[k] = a.squash == 2 ? a.sq_lo[k] + (t0 + 1.0f) * a.sq_half[k] : t0;
+              }
+              if (k + 1 < a.A) {
+                const float t1 = tanhf(u1);
+                env[k + 1] = a.squash == 2 ? a.sq_lo[k + 1] + (t1 + 1.0f) * a.sq_half[k + 1] : t1;
+              }
+            }
           }
         }
       }
@@ -595,9 +615,21 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
 
 int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                void* actions, int64_t n, uint64_t seed, uint64_t counter, hipStream_t s,
-               float* heads) {
+               float* heads, const ActSquash* squash) {
   if (n <= 0) return DPPO_OK;
   ActArgs k{};
+  if (squash && squash->env_actions) {
+    if (!sh.continuous || sh.A > 16) {
+      set_error("tanh squash needs a continuous action space of at most 16 dims");
+      return DPPO_EINVAL;
+    }
+    k.env_act = squash->env_actions;
+    k.squash = squash->low && squash->high ? 2 : 1;
+    for (int j = 0; j < sh.A && k.squash == 2; ++j) {
+      k.sq_lo[j] = squash->low[j];
+      k.sq_half[j] = 0.5f * (squash->high[j] - squash->low[j]);
+    }
+  }
   k.L = make_layout(sh);
   k.po = po;
   k.params = params;

@@ -50,8 +50,14 @@ constexpr uint32_t kLower = 0x7FFFFFFFu;
 // One MT19937 block: twist the 624-word state and temper it into out[].  The three twist
 // ranges only depend on words at distance >= 227 (or the block before), so each loop
 // vectorises; AVX2 clones are picked at load time where the host has them.
-__attribute__((target_clones("avx512f", "avx2", "default"))) void twist_block(uint32_t* __restrict mt,
-                                                                   uint32_t* __restrict out) {
+// (The sanitizer builds, DPPO_SANITIZE, compile one plain version: an ifunc resolver runs during
+// relocation, before the sanitizer runtime is up, and its instrumented code crashes there.)
+#ifdef DPPO_SANITIZE
+#define DPPO_TWIST_CLONES
+#else
+#define DPPO_TWIST_CLONES __attribute__((target_clones("avx512f", "avx2", "default")))
+#endif
+DPPO_TWIST_CLONES void twist_block(uint32_t* __restrict mt, uint32_t* __restrict out) {
   int i = 0;
   for (; i < kN - kM; ++i) {
     uint32_t y = (mt[i] & kUpper) | (mt[i + 1] & kLower);
@@ -336,6 +342,10 @@ int main_thread_cpu() {
 bool l3_domain(int mode, cpu_set_t* out) {
   cpu_set_t allowed;
   if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+  if (mode == 3) {  // every allowed CPU (tests: the pooled path without a cache topology)
+    *out = allowed;
+    return CPU_COUNT(&allowed) >= 1;
+  }
   const int home = sched_getcpu();
   if (mode == 1) return home >= 0 && l3_of(home, allowed, out) && CPU_ISSET(home, out);
   const int mcpu = main_thread_cpu();
@@ -499,6 +509,8 @@ struct PermTicket {
 };
 std::mutex g_scratch_mu;
 std::vector<std::vector<int32_t>> g_scratch_free;
+// calls of perm_start, of those on the swap pool, of those with the producer ring (dppo_perm_stats)
+std::atomic<int64_t> g_calls{0}, g_pooled{0}, g_ringed{0};
 
 std::vector<int32_t> take_scratch(size_t n) {
   std::lock_guard<std::mutex> g(g_scratch_mu);
@@ -552,6 +564,9 @@ int perm_start(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* o
   std::unique_ptr<RingBlocks> ring;
   if (t->pooled && ring_mode && n * count >= (1 << 20))
     ring.reset(new RingBlocks(g.mt, SwapPool::get().cpus()));
+  g_calls.fetch_add(1, std::memory_order_relaxed);
+  if (t->pooled) g_pooled.fetch_add(1, std::memory_order_relaxed);
+  if (ring) g_ringed.fetch_add(1, std::memory_order_relaxed);
   LocalBlocks local{g};
   const uint32_t* blk = g.out;
   int p = g.pos;
@@ -596,6 +611,14 @@ extern "C" int dppo_perm_numpy_async(uint32_t* key, int32_t* pos, int64_t n, int
   const int rc = perm_start(key, pos, n, count, out, t);
   *ticket = t;
   return rc;
+}
+
+extern "C" int dppo_perm_stats(int64_t* out3) {
+  if (!out3) return DPPO_EINVAL;
+  out3[0] = g_calls.load();
+  out3[1] = g_pooled.load();
+  out3[2] = g_ringed.load();
+  return DPPO_OK;
 }
 
 extern "C" int dppo_perm_wait(void* ticket) {

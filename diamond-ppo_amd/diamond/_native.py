@@ -25,11 +25,12 @@ PERM_SLOTS = 3  # pinned permutation staging slots per handle (include/dppo.h DP
 
 EXPORTED = [
     "dppo_version", "dppo_last_error", "dppo_param_layout", "dppo_create", "dppo_destroy",
-    "dppo_gae_f32", "dppo_adv_stats", "dppo_adv_normalize_f32", "dppo_old_policy_f32",
+    "dppo_gae_f32", "dppo_adv_stats", "dppo_adv_sums", "dppo_adv_stats_from_sums",
+    "dppo_adv_normalize_f32", "dppo_old_policy_f32",
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_resolve", "dppo_act_f32", "dppo_loopback_group",
+    "dppo_perm_targets_numpy", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
@@ -96,8 +97,12 @@ def load():
         "dppo_gae_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
         "dppo_adv_stats": (ctypes.c_int, [vp, vp, vp]),
         "dppo_adv_normalize_f32": (ctypes.c_int, [vp, vp, i64, vp]),
+        "dppo_adv_sums": (ctypes.c_int, [vp, vp, vp]),
+        "dppo_adv_stats_from_sums": (ctypes.c_int, [vp, f64, vp, vp]),
         "dppo_old_policy_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
         "dppo_act_f32": (ctypes.c_int, [vp, vp, vp, i64, ctypes.c_uint64, ctypes.c_uint64, vp, vp]),
+        "dppo_act_squash_f32": (ctypes.c_int, [vp, vp, vp, i64, ctypes.c_uint64, ctypes.c_uint64,
+                                               vp, vp, vp, vp, vp]),
         "dppo_learn_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,
                                           P(LearnOutputs), vp]),
         "dppo_learn_targets_f32": (ctypes.c_int, [vp, P(Rollout), vp, vp, vp, P(HParams), vp,
@@ -112,6 +117,7 @@ def load():
         "dppo_perm_targets_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
         "dppo_perm_numpy_async": (ctypes.c_int, [vp, P(i32), i64, i32, vp, P(vp)]),
         "dppo_perm_wait": (ctypes.c_int, [vp]),
+        "dppo_perm_stats": (ctypes.c_int, [P(i64)]),
         "dppo_perm_resolve": (ctypes.c_int, [vp, vp, i64, i32, vp, vp]),
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
@@ -195,6 +201,13 @@ def perm_wait(ticket) -> None:
     check(load().dppo_perm_wait(ticket), "dppo_perm_wait")
 
 
+def perm_stats() -> dict:
+    """{calls, pooled, ring}: host permutation draws so far, on the swap pool, with the ring."""
+    out = (ctypes.c_int64 * 3)()
+    check(load().dppo_perm_stats(out), "dppo_perm_stats")
+    return {"calls": out[0], "pooled": out[1], "ring": out[2]}
+
+
 def perm_targets_numpy(key: np.ndarray, pos: int, n: int, count: int,
                        out: np.ndarray | int) -> int:
     """The MT19937 half of :func:`perm_numpy`: Fisher-Yates swap targets ``out[c][i] = j_i``
@@ -259,7 +272,8 @@ class Handle:
             pass
 
     def perm_buffer(self, slot: int = 0) -> int:
-        """Pinned [E][B] int32 staging slot 0/1 (waits for its previous upload)."""
+        """Pinned [E][B] int32 staging slot ``slot`` (0 .. PERM_SLOTS-1); waits, on the calling
+        thread, for the slot's previous upload."""
         p = ctypes.c_void_p()
         check(self.lib.dppo_perm_buffer(self.h, int(slot), ctypes.byref(p)), "dppo_perm_buffer")
         return p.value

@@ -8,7 +8,9 @@ anywhere in the reference: continuous_ppo.py:83-111,276-277).
 
 ``ContinuousPPOConfig.tanh_squash`` (default False, an extension beyond the reference; SURVEY §8
 f2) makes ``rollout()`` send ``a = tanh(u)`` -- rescaled to the action space's bounds when they
-are finite -- to the environment while the experience keeps the Gaussian sample ``u``.  The
+are finite -- to the environment while the experience keeps the Gaussian sample ``u``.  With the
+default network the squash is computed on the device by the same act-kernel launch that draws
+``u`` (``dppo_act_squash_f32``); a custom ``network_cls`` squashes on the host.  The
 squashed policy's log-density is ``log N(u) - sum log(1 - tanh(u)^2)`` (:func:`squashed_log_prob`);
 the correction does not depend on the parameters, so it cancels in the PPO ratio and the update
 is exactly the unsquashed Gaussian update on ``u`` -- the same fused kernels, no second path.  The
@@ -148,3 +150,15 @@ class ContinuousPPO(_AgentBase):
         if getattr(self.cfg, "tanh_squash", False):
             return squash_to_space(actions, self.envs.single_action_space)
         return actions
+
+    def _squash_spec(self):
+        """tanh_squash with the fused sampler: the squash runs in the act kernel
+        (dppo_act_squash_f32) -- (low, high) for a Box with finite bounds, else plain tanh."""
+        if not getattr(self.cfg, "tanh_squash", False):
+            return None
+        sp = self.envs.single_action_space
+        low = np.asarray(getattr(sp, "low", -1.0), dtype=np.float64)
+        high = np.asarray(getattr(sp, "high", 1.0), dtype=np.float64)
+        if np.all(np.isfinite(low)) and np.all(np.isfinite(high)):
+            return (low, high)
+        return True

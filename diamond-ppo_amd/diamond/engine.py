@@ -297,16 +297,28 @@ class _DraftWorker:
             self._jobs.append((fn, done))
             self._cv.notify()
 
+    def stop(self, timeout: float = 60.0):
+        """Run what is queued, then end the thread (a None job is the stop mark)."""
+        with self._cv:
+            self._jobs.append((None, None))
+            self._cv.notify()
+        if threading.current_thread() is not self._thread:
+            self._thread.join(timeout)
+
     def _run(self):
         while True:
             with self._cv:
                 while not self._jobs:
                     self._cv.wait()
                 fn, done = self._jobs.popleft()
+            if fn is None:
+                return
             try:
                 fn()
             finally:
                 done.set()
+            # the finished job's closure must not outlive it: it holds the draft's buffers
+            del fn, done
 
 
 class NativeLearner:
@@ -347,7 +359,10 @@ class NativeLearner:
         self.m, self.v = bind_adam_state(optimizer, self.flat)
         self.optimizer = optimizer
         self.network = network
-        if self.world > 1:
+        # DPPO_FORCE_COMM=1: an RCCL communicator even for one rank, so learn() runs the
+        # collective sequence (slab reduce -> ncclAllReduce -> clip + Adam) -- how the RCCL path
+        # is exercised on a one-GPU box
+        if self.world > 1 or os.environ.get("DPPO_FORCE_COMM") == "1":
             self._init_comm()
         self.last_trace = None
         # host-side seconds of learn(), reported by bench.py.  Launching thread: "perms" (waiting
@@ -373,9 +388,13 @@ class NativeLearner:
         self.draft_depth = max(1, min(2, int(os.environ.get("DPPO_PERM_DEPTH", "2"))))
         self._slot = 0
         self._worker = None
+        self._closed = False
 
     def _init_comm(self):
         d = torch.distributed
+        if not (d.is_available() and d.is_initialized()):   # one rank, no process group
+            self.handle.comm_init(1, 0, N.comm_unique_id())
+            return
         obj = [N.comm_unique_id() if self.rank == 0 else None]
         d.broadcast_object_list(obj, src=0)
         self.handle.comm_init(self.world, self.rank, obj[0])
@@ -388,13 +407,19 @@ class NativeLearner:
             self.flat.flat.copy_(cpu)
 
     # -----------------------------------------------------------------------------------------
-    def act(self, observations: np.ndarray, seed: int) -> np.ndarray:
+    def act(self, observations: np.ndarray, seed: int, squash=None):
         """Sample actions for a batch of observations with the fused actor kernel
         (``dppo_act_f32``; default network only): pinned upload, one launch, pinned download.
         Discrete actions come back int64 like the reference's ``Categorical.sample().numpy()``;
-        continuous ones float32 ``[n, A]``."""
+        continuous ones float32 ``[n, A]``.
+
+        ``squash`` (continuous only, the tanh-squash extension): ``True`` for tanh(u), or a
+        ``(low, high)`` pair of A-float bounds; then the same kernel launch also emits the
+        environment's actions (``dppo_act_squash_f32``) and ``(u, env_actions)`` is returned."""
         if not self.fused:
             raise RuntimeError("act() needs the default network (fused path)")
+        if squash is not None and squash is not False:
+            return self._act_squash(observations, seed, squash)
         obs = np.asarray(observations, dtype=np.float32).reshape(-1, self.D)
         n = obs.shape[0]
         b = getattr(self, "_act_bufs", None)
@@ -419,6 +444,38 @@ class NativeLearner:
         out = b["act_h"].numpy()
         return out.copy() if self.continuous else out.astype(np.int64)
 
+    def _act_squash(self, observations, seed, squash):
+        if not self.continuous:
+            raise ValueError("tanh squash needs a continuous action space")
+        obs = np.asarray(observations, dtype=np.float32).reshape(-1, self.D)
+        n = obs.shape[0]
+        b = getattr(self, "_sq_bufs", None)
+        if b is None or b["n"] != n:
+            b = {"n": n, "obs_h": torch.empty((n, self.D), dtype=torch.float32).pin_memory(),
+                 "obs_d": torch.empty((n, self.D), dtype=torch.float32, device=self.device),
+                 "out_d": torch.empty((2, n, self.A), dtype=torch.float32, device=self.device),
+                 "out_h": torch.empty((2, n, self.A), dtype=torch.float32).pin_memory()}
+            self._sq_bufs = b
+        if squash is True:
+            lo = hi = None
+        else:
+            lo = np.ascontiguousarray(np.broadcast_to(squash[0], (self.A,)), np.float32)
+            hi = np.ascontiguousarray(np.broadcast_to(squash[1], (self.A,)), np.float32)
+        b["obs_h"].numpy()[:] = obs
+        b["obs_d"].copy_(b["obs_h"], non_blocking=True)
+        s = torch.cuda.current_stream(self.device)
+        # call counter of this sampler (one Philox draw per sample and call, as act())
+        counter = self.__dict__.setdefault("_sq_counter", 0)
+        N.check(self.handle.lib.dppo_act_squash_f32(
+            self.handle.h, self.flat.flat.data_ptr(), b["obs_d"].data_ptr(), n,
+            seed & (2 ** 64 - 1), counter, N.ptr(lo), N.ptr(hi), b["out_d"][0].data_ptr(),
+            b["out_d"][1].data_ptr(), s.cuda_stream), "dppo_act_squash_f32")
+        self._sq_counter += 1
+        b["out_h"].copy_(b["out_d"], non_blocking=True)
+        s.synchronize()
+        out = b["out_h"].numpy()
+        return out[0].copy(), out[1].copy()
+
     def _start_draft(self, key: np.ndarray | None, pos: int | None):
         """Queue the draws of one more learn's permutations (or swap targets) on the draft worker
         thread, starting from (key, pos) -- or, when None, from the final state of the draft
@@ -429,6 +486,9 @@ class NativeLearner:
         d = {"slot": slot, "key_in": None if key is None else key.copy(), "pos_in": pos,
              "ok": False, "device": self.device_shuffle, "done": threading.Event()}
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
+        # the job closes over plain values, not the learner: a queued or finished job never keeps
+        # the learner (and its handle's pinned slots) alive
+        device_shuffle, perm_n, epochs = self.device_shuffle, self.perm_n, self.cfg.num_epochs
 
         # The slot's previous upload must be done before the draws overwrite it: waited for here,
         # on the launching thread (device back-pressure), not on the draft thread -- a HIP wait
@@ -444,13 +504,13 @@ class NativeLearner:
                 d["key_in"], d["pos_in"] = prev["key_out"].copy(), prev["pos_out"]
             t1 = time.perf_counter()
             k = d["key_in"].copy()
-            if self.device_shuffle:
-                d["pos_out"] = draw(k, d["pos_in"], self.perm_n, self.cfg.num_epochs, buf)
+            if device_shuffle:
+                d["pos_out"] = draw(k, d["pos_in"], perm_n, epochs, buf)
             else:
                 # returns after the draws: the last epochs' swaps finish on the host pool while
                 # the next draft's draws (chained on key_out) already run
-                d["pos_out"], d["ticket"] = N.perm_numpy_async(k, d["pos_in"], self.perm_n,
-                                                               self.cfg.num_epochs, buf)
+                d["pos_out"], d["ticket"] = N.perm_numpy_async(k, d["pos_in"], perm_n, epochs,
+                                                               buf)
             d["key_out"] = k
             d["t_draw"] = time.perf_counter() - t1
             d["ok"] = True
@@ -472,6 +532,28 @@ class NativeLearner:
         """Wait for every queued draft (their slots are being written) and drop them."""
         while self._drafts:
             self._finish(self._drafts.popleft())
+
+    def close(self):
+        """Release the handle safely: first every queued draft and the host-pool swaps still
+        writing its pinned permutation slots, then the draft thread, then the device workspace
+        (dppo_destroy frees the pinned slots).  Idempotent; also run when the learner is
+        garbage-collected."""
+        if getattr(self, "_closed", True):
+            return
+        self._closed = True
+        try:
+            self._drain_drafts()
+        finally:
+            if self._worker is not None:
+                self._worker.stop()
+                self._worker = None
+            self.handle.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def _targets(self):
         """This learn's permutations (or, with device_shuffle, their swap targets) in a pinned

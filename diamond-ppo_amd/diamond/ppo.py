@@ -164,6 +164,10 @@ class _AgentBase:
         tanh_squash option overrides it).  The experience always keeps ``actions``."""
         return actions
 
+    def _squash_spec(self):
+        """None (the env gets the sampled actions), or the fused sampler's squash argument."""
+        return None
+
     # -- drop-in surface ------------------------------------------------------------------------
     def rollout(self) -> list[list[np.ndarray]]:
         """Collect one rollout across the vector env (reference ppo.py:153-186).  Each step is
@@ -174,13 +178,20 @@ class _AgentBase:
         stager = self._rollout_stager()
         if stager is not None:
             stager.begin()
+        squash = self._squash_spec()
         for t in range(self.cfg.rollout_steps):
             if self.fused_actions and self._learner.fused:
-                actions = self._learner.act(observations, self._act_seed)
+                if squash is None:
+                    actions = self._learner.act(observations, self._act_seed)
+                    env_actions = actions
+                else:  # the env action comes out of the same kernel launch
+                    actions, env_actions = self._learner.act(observations, self._act_seed,
+                                                             squash=squash)
             else:
                 actions = self.network.get_actions(observations, device=self.device)
+                env_actions = self._env_actions(actions)
             next_observations, rewards, terminations, truncations, infos = self.envs.step(
-                self._env_actions(actions))
+                env_actions)
             experience.append([observations, next_observations, actions, rewards, terminations,
                                truncations])
             if stager is not None:
@@ -264,6 +275,13 @@ class _AgentBase:
     def learn_trace(self) -> np.ndarray:
         """[E*M, 5] {loss, loss_policy, loss_value, entropy, grad_norm} of the last learn()."""
         return self._learner.trace()
+
+    def close(self) -> None:
+        """Release the agent's device workspace now (also done when it is garbage-collected):
+        waits for the look-ahead permutation drafts still writing its pinned slots first."""
+        self._learner.close()
+        for h in self.__dict__.get("_gae_handles", {}).values():
+            h.close()
 
     def load_checkpoint(self, path) -> None:
         """Checkpointer.load + re-binding of the Adam state to the kernels' flat buffers."""

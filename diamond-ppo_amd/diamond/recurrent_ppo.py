@@ -8,6 +8,13 @@ log-probs / values / next-values cached during rollout (:219-243), and ``learn``
 full [T, N] sequence from the stored initial ``hx`` for every minibatch (:337-341).  The network
 runs under torch autograd on the GPU; GAE, advantage normalisation and clip + Adam run in the
 gfx950 kernels.  No oracle pins this path beyond the shared GAE (reference broken).
+
+Data parallelism (torchrun, one process per GPU): each rank owns its own envs (seeded
+``seed + rank * num_envs``) and permutes its own samples (``np.random`` seeded ``seed + rank``);
+global minibatch j is the union of the ranks' local minibatches j.  The advantage statistics are
+global (the ranks' {sum, sum^2} all-reduced, ppo.py:243 over the global batch), each rank's loss
+is its local mean scaled by 1/world, and the flat gradient is all-reduced (SUM, RCCL under the
+"nccl" backend) before the replicated clip + Adam -- so every rank takes the identical step.
 """
 from __future__ import annotations
 
@@ -117,7 +124,7 @@ class RecurrentPPO:
         world, rank = dist_world()
         if cfg.seed is not None:
             np.random.seed(cfg.seed + rank)
-            torch.manual_seed(cfg.seed)
+            torch.manual_seed(cfg.seed)   # same initial weights on every rank
         self.envs = envs if envs is not None else make_vector_env(env_fn, cfg.num_envs)
         obs_space, act_space = self.envs.single_observation_space, self.envs.single_action_space
         self.network = network_cls(obs_space, act_space, cfg=cfg)
@@ -135,6 +142,14 @@ class RecurrentPPO:
                       num_epochs=cfg.num_epochs, num_minibatches=cfg.num_minibatches,
                       world_size=1, rank=0)
         self.handle = N.Handle(self.device.index or 0, dims)
+        if world > 1:   # replicate rank 0's initial weights (identical seeds: a no-op in practice)
+            d = torch.distributed
+            if d.get_backend() == "nccl":
+                d.broadcast(self.flat.flat, src=0)
+            else:
+                cpu = self.flat.flat.cpu()
+                d.broadcast(cpu, src=0)
+                self.flat.flat.copy_(cpu)
         self.logger, self.timer = Logger(), Timer()
         self.checkpointer = Checkpointer(folder="models", run_name="default")
         self.ticker = Ticker(cfg.total_steps, cfg.num_envs, cfg.rollout_steps, verbose=cfg.verbose)
@@ -200,9 +215,19 @@ class RecurrentPPO:
                                               np.asarray(truncs), values, next_values)
         returns = values + advantages
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        world, _ = dist_world()
         if cfg.advantage_norm:
             ms = torch.empty(4, dtype=torch.float32, device=self.device)
-            N.check(lib.dppo_adv_stats(h, ms.data_ptr(), stream), "dppo_adv_stats")
+            if world > 1:
+                # global statistics: this rank's {sum, sum^2}, all-reduced, then finalised
+                sums = torch.empty(2, dtype=torch.float64, device=self.device)
+                N.check(lib.dppo_adv_sums(h, sums.data_ptr(), stream), "dppo_adv_sums")
+                torch.distributed.all_reduce(sums)
+                n_total = float(cfg.rollout_steps * cfg.num_envs * world)
+                N.check(lib.dppo_adv_stats_from_sums(sums.data_ptr(), n_total, ms.data_ptr(),
+                                                     stream), "dppo_adv_stats_from_sums")
+            else:
+                N.check(lib.dppo_adv_stats(h, ms.data_ptr(), stream), "dppo_adv_stats")
             advantages = advantages.contiguous()
             N.check(lib.dppo_adv_normalize_f32(advantages.data_ptr(), ms.data_ptr(),
                                                advantages.numel(), stream), "normalize")
@@ -229,7 +254,12 @@ class RecurrentPPO:
                                                               1 + cfg.ppo_clip)).mean()
                 l_v = 0.5 * torch.nn.functional.mse_loss(nv, returns[mb_idx])
                 loss = l_pi + cfg.value_loss_weight * l_v - cfg.entropy_beta * dist.entropy().mean()
+                if world > 1:
+                    # local mean x 1/world, summed over the ranks = the union minibatch's mean
+                    loss = loss * (1.0 / world)
                 loss.backward()
+                if world > 1:
+                    torch.distributed.all_reduce(self.flat.grad)
                 step += 1
                 N.check(lib.dppo_clip_adam_f32(
                     self.flat.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),

@@ -131,6 +131,13 @@ int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, cons
  * all ranks when a communicator is attached); writes device float mean_std[2]. */
 int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream);
 
+/* The pieces of dppo_adv_stats for a caller that does its own exchange (RecurrentPPO under
+ * torch.distributed): dppo_adv_sums writes this rank's {sum adv, sum adv^2} of the last
+ * dppo_gae_f32 as device double[2]; after the caller's all-reduce, dppo_adv_stats_from_sums turns
+ * the global sums of n_total advantages into the mean and unbiased std (ppo.py:243). */
+int dppo_adv_sums(dppo_handle* h, double* sums, void* stream);
+int dppo_adv_stats_from_sums(const double* sums, double n_total, float* mean_std, void* stream);
+
 /* adv = (adv - mean) / (std + 1e-6) in place (ppo.py:243). */
 int dppo_adv_normalize_f32(float* adv, const float* mean_std, int64_t n, void* stream);
 
@@ -150,6 +157,16 @@ int dppo_old_policy_f32(dppo_handle* h, const float* params, const float* obs, c
  * advance `counter` once per call. */
 int dppo_act_f32(dppo_handle* h, const float* params, const float* obs, int64_t n, uint64_t seed,
                  uint64_t counter, void* actions, void* stream);
+
+/* dppo_act_f32 for a continuous action space, plus the action the environment receives under
+ * the tanh-squash option (an extension -- the reference sends the raw Gaussian
+ * sample, continuous_ppo.py:83-93): actions [n][A] = the Gaussian samples u (the same draws as
+ * dppo_act_f32 for this seed / counter; the experience keeps them), env_actions [n][A] =
+ * low + (tanh(u) + 1) * (high - low) / 2 with low/high host arrays of A finite floats (high > low),
+ * or tanh(u) when both are NULL. */
+int dppo_act_squash_f32(dppo_handle* h, const float* params, const float* obs, int64_t n,
+                        uint64_t seed, uint64_t counter, const float* low, const float* high,
+                        float* actions, float* env_actions, void* stream);
 
 /* The actor half of dppo_act_f32 without the draw: the logits (discrete, ppo.py:79) or Gaussian
  * means (continuous, continuous_ppo.py:88-90) of the default actor for obs [n][D], written to
@@ -233,6 +250,11 @@ int dppo_perm_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32
 int dppo_perm_numpy_async(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out,
                           void** ticket);
 int dppo_perm_wait(void* ticket);
+
+/* Counters of the host permutation draws since load: {calls, calls whose Fisher-Yates swaps ran
+ * on the pinned swap pool, calls whose MT19937 blocks came from the producer thread's ring}.
+ * DPPO_PERM_PIN=3 pins the pool to every allowed CPU (no cache-topology lookup). */
+int dppo_perm_stats(int64_t* out3);
 
 /* The MT19937 half of dppo_perm_numpy: the Fisher-Yates swap targets out[c][i] = j_i
  * (i = n-1 .. 1; out[c][0] = 0) of `count` successive permutations, advancing key/pos exactly

@@ -38,5 +38,5 @@ def load_golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
 
 
-LEARN_TRACES = ["cartpole_small", "cartpole_decay", "lunar_medium", "lunar_noadvnorm",
+LEARN_TRACES = ["cartpole_small", "cartpole_decay", "cartpole_c1", "lunar_medium", "lunar_noadvnorm",
                 "cheetah_small", "pendulum_medium"]

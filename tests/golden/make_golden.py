@@ -17,6 +17,7 @@ What is captured (SURVEY.md §8(c) "Golden vectors to generate & commit"):
                         gradients, total grad norm, parameters after every optimizer step, final
                         Adam state.  Some traces call learn() twice (Adam step / RNG continuation,
                         decay_lr).
+* learn_cartpole_c1.npz -- BASELINE configs[0] (CartPole, T=128, N=8) at full size.
 * perm_seed42.npz    -- numpy legacy RandomState permutations (ppo.py:120-122,254).
 * ckpt_cartpole-step000128.pt + ckpt_cartpole_resume.npz -- a checkpoint written by the
                         reference's Checkpointer.save after one learn(), and the learn() of a fresh
@@ -358,6 +359,9 @@ def main():
     if sys.argv[1:] == ["checkpoint"]:
         make_checkpoint_fixture(diamond, gym_stub)
         return
+    if sys.argv[1:] == ["c1"]:
+        make_c1_trace(diamond, gym_stub)
+        return
     make_checkpoint_fixture(diamond, gym_stub)
     make_perm_golden()
     make_gae_cases(diamond, gym_stub)
@@ -375,6 +379,15 @@ def main():
                      n_learn=2, p_term=0.0, p_trunc=0.05)
     make_learn_trace(diamond, gym_stub, "pendulum_medium", continuous=True, T=32, N=32, D=3, A=1,
                      p_term=0.0, p_trunc=0.01, save_all_grads=False)
+    make_c1_trace(diamond, gym_stub)
+
+
+def make_c1_trace(diamond, gym_stub):
+    """BASELINE configs[0] at its own size: CartPole PPO, T=128 x N=8 (B=1,024, minibatches of
+    128), the reference's defaults otherwise (ppo.py:15-37), SURVEY 8(d) done rates; two learn()
+    calls (Adam and RNG continuation)."""
+    make_learn_trace(diamond, gym_stub, "cartpole_c1", continuous=False, T=128, N=8, D=4, A=2,
+                     n_learn=2, p_term=0.02, p_trunc=0.005)
 
 
 if __name__ == "__main__":

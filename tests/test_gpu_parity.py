@@ -304,6 +304,36 @@ def test_learn_is_deterministic():
     assert np.array_equal(res[0], res[1])
 
 
+def test_agent_teardown_drains_permutation_drafts():
+    """An agent dropped right after a learn() (its look-ahead drafts still queued or swapping on
+    the host pool into the handle's pinned slots) is garbage-collected: the learner drains the
+    drafts before dppo_destroy frees the slots, its draft thread ends, and the next agent works.
+    Also explicit close() on a live agent, twice."""
+    import gc
+    import weakref
+    z = load_golden("learn_lunar_medium.npz")
+    results = []
+    for k in range(3):
+        agent = make_agent(z)
+        np.random.seed(21)
+        agent.learn(experience(z, 0))
+        assert agent._learner._drafts            # drafts for the next learns are in flight
+        results.append(flat_params(agent))
+        worker = agent._learner._worker
+        if k == 2:
+            agent.close()
+            agent.close()
+            assert not worker._thread.is_alive()
+            continue
+        ref = weakref.ref(agent._learner)
+        del agent
+        gc.collect()
+        assert ref() is None, "the learner was kept alive"
+        worker._thread.join(30)
+        assert not worker._thread.is_alive()
+    assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
+
+
 def test_indivisible_minibatch_raises_value_error():
     import gym_stub
     cfg = diamond.PPOConfig(rollout_steps=3, num_envs=5, num_minibatches=4, verbose=False)
@@ -367,9 +397,11 @@ def test_permutation_lookahead_hit_and_miss(device_shuffle):
 # ---------------------------------------------------------------------------------------------
 def test_tanh_squash_rollout_and_learn():
     """ContinuousPPOConfig.tanh_squash (extension): the env receives tanh(u) rescaled
-    to the Box bounds, the experience keeps the Gaussian sample u, and learn() on that experience
-    is bit-identical to the unsquashed agent's learn() on the same experience (the squash's
+    to the Box bounds -- computed on the device by the act kernel -- and checked against the
+    oracle's squash_action of the experience's Gaussian samples u; learn() on that experience is
+    bit-identical to the unsquashed agent's learn() on the same experience (the squash's
     log-density correction does not depend on the parameters)."""
+    from oracle import ppo_np as P
     import gym_stub
 
     class RecordingEnvs(gym_stub.SyncVectorEnv):
@@ -396,8 +428,7 @@ def test_tanh_squash_rollout_and_learn():
         sent = np.stack(envs.sent)
         if squash:
             assert np.all(np.abs(sent) <= 2.0)
-            np.testing.assert_allclose(sent, (-2.0 + (np.tanh(u) + 1.0) * 2.0).astype(np.float32),
-                                       rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(sent, P.squash_action(u, -2.0, 2.0), rtol=0, atol=2e-6)
             assert not np.allclose(sent, u)
             squashed_exp = exp
         else:

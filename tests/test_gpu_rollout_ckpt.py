@@ -110,18 +110,84 @@ def test_fused_draws_are_the_documented_philox_stream(cont):
         assert clear.mean() > 0.99
         assert np.array_equal(got[clear], want[clear])
     else:
-        ls = params["actor_log_std"].astype(np.float64).reshape(A)
-        want = np.empty((n, A))
-        for k0 in range(0, A, 4):
-            c = philox4x32_10((i & M32, (i >> np.uint64(32)) ^ np.uint64(k0 << 24),
-                               np.full(n, counter), np.zeros(n)), key)
-            for pp in range(2):
-                r = np.sqrt(-2.0 * np.log(u01(c[2 * pp])))
-                th = 2 * np.pi * u01(c[2 * pp + 1])
-                for kk, val in ((k0 + 2 * pp, r * np.cos(th)), (k0 + 2 * pp + 1, r * np.sin(th))):
-                    if kk < A:
-                        want[:, kk] = out[:, kk] + np.exp(ls[kk]) * val
+        want = oracle_gaussian_draws(out, params["actor_log_std"], seed, counter)
         np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4)
+
+
+def oracle_gaussian_draws(out, log_std, seed, counter):
+    """The continuous sampler's draws restated: mean + exp(log_std) * Box-Muller on the Philox
+    stream (pairs (c0,c1), (c2,c3) per block of 4 action dims, block k0 xor-ed into the counter's
+    high word), from the oracle's means ``out`` [n][A]."""
+    n, A = out.shape
+    key = (seed & 0xFFFFFFFF, seed >> 32)
+    i = np.arange(n, dtype=np.uint64)
+    ls = np.asarray(log_std, np.float64).reshape(A)
+    want = np.empty((n, A))
+    for k0 in range(0, A, 4):
+        c = philox4x32_10((i & M32, (i >> np.uint64(32)) ^ np.uint64(k0 << 24),
+                           np.full(n, counter), np.zeros(n)), key)
+        for pp in range(2):
+            r = np.sqrt(-2.0 * np.log(u01(c[2 * pp])))
+            th = 2 * np.pi * u01(c[2 * pp + 1])
+            for kk, val in ((k0 + 2 * pp, r * np.cos(th)), (k0 + 2 * pp + 1, r * np.sin(th))):
+                if kk < A:
+                    want[:, kk] = out[:, kk] + np.exp(ls[kk]) * val
+    return want
+
+
+@pytest.mark.parametrize("name,bounded", [("cheetah_small", True), ("cheetah_small", False),
+                                          ("pendulum_medium", True)])
+def test_device_tanh_squash_matches_oracle(name, bounded):
+    """f2 on the device: dppo_act_squash_f32 draws the Gaussian samples u (the same stream as
+    dppo_act_f32) and, in the same launch, the environment's actions.  Both against the oracle:
+    u against the Philox restatement on the oracle's means, the env actions against
+    oracle.ppo_np.squash_action on the oracle's samples (tolerance: the samples' 1e-4 through
+    tanh' <= 1 and the half-range) and, tightly, on the device's own samples."""
+    z = load_golden(f"learn_{name}.npz")
+    T, Nn, D, A, _, _ = (int(x) for x in z["dims"])
+    agent = make_agent(z)
+    L = agent._learner
+    obs = np.ascontiguousarray(z["exp0/obs"].reshape(T * Nn, D), np.float32)
+    n = obs.shape[0]
+    params = {k: z["init/" + k] for k in z["param_names"]}
+    with torch.no_grad():   # wider samples, so tanh's saturated tails are exercised
+        agent.network.actor_log_std.fill_(0.7)
+    params["actor_log_std"] = np.full((1, A), 0.7, np.float32)
+    if bounded:
+        lo = np.linspace(-2.0, -0.25, A).astype(np.float32)
+        hi = np.linspace(0.5, 3.0, A).astype(np.float32)
+    o = torch.from_numpy(obs).to(dev())
+    u = torch.empty((n, A), device=dev())
+    env = torch.empty((n, A), device=dev())
+    seed, counter = 0xBEEF_0000_1234_5678, 3
+    N.check(L.handle.lib.dppo_act_squash_f32(
+        L.handle.h, L.flat.flat.data_ptr(), o.data_ptr(), n, seed, counter,
+        lo.ctypes.data if bounded else None, hi.ctypes.data if bounded else None, u.data_ptr(),
+        env.data_ptr(), stream()))
+    torch.cuda.synchronize()
+    u, env = u.cpu().numpy(), env.cpu().numpy()
+    u_want = oracle_gaussian_draws(P.forward(params, obs, True)["out"].astype(np.float64),
+                                   params["actor_log_std"], seed, counter)
+    np.testing.assert_allclose(u, u_want, rtol=1e-4, atol=1e-4)
+    if bounded:
+        half = 0.5 * (hi.astype(np.float64) - lo)
+        env_want = P.squash_action(u_want, lo.astype(np.float64), hi.astype(np.float64))
+        env_own = P.squash_action(u, lo.astype(np.float64), hi.astype(np.float64))
+        assert np.all(env >= lo) and np.all(env <= hi)
+    else:
+        half = np.ones(A)
+        env_want, env_own = np.tanh(u_want), np.tanh(u.astype(np.float64))
+        assert np.all(np.abs(env) <= 1.0)
+    np.testing.assert_allclose(env, env_want, rtol=0, atol=float(1e-4 * half.max() + 1e-6))
+    np.testing.assert_allclose(env, env_own, rtol=0, atol=float(4e-7 * (1 + np.abs(lo).max() if
+                                                                        bounded else 1)))
+    assert (np.abs(u) > 3).any()  # saturated tails were drawn
+    # and the same u as the unsquashed sampler for this (seed, counter)
+    u2 = torch.empty((n, A), device=dev())
+    N.check(L.handle.lib.dppo_act_f32(L.handle.h, L.flat.flat.data_ptr(), o.data_ptr(), n, seed,
+                                      counter, u2.data_ptr(), stream()))
+    torch.cuda.synchronize()
+    assert np.array_equal(u, u2.cpu().numpy())
 
 
 def test_resume_from_reference_checkpoint():
