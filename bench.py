@@ -26,7 +26,8 @@ start/end HIP events (libdppo timing mode): ``kernels``, ``device_ms_per_step`` 
 come from it, never the throughput.  At N = 1 the line also carries ``configs_extra`` (C3
 LunarLander 8192, C4 HalfCheetah 4096 and C5's 65,536 envs on one GPU -- the strong-scaling
 anchor), ``roofline_gae`` (the GAE kernel at num_envs = 8192 over 16 rotating buffer sets, 368 MB
-> the 256 MB Infinity Cache) and ``cpu_baseline``: the PyTorch-CPU restatement of the reference
+> the 256 MB Infinity Cache; ``roofline_gae_affine`` the tolerance-mode kernel, and
+``roofline_gae_65536`` both at C5's one-GPU 65,536 envs) and ``cpu_baseline``: the PyTorch-CPU restatement of the reference
 path (oracle/ppo_torch.py) timed for one full learn() on the host cores, with the NumPy oracle
 beside it as ``cpu_baseline_numpy``.
 """
@@ -104,12 +105,19 @@ def synth_rollout(T, N, D, A, continuous, p_term, p_trunc, seed, device):
     return DeviceRollout(g(obs), g(nobs), g(act), g(rew), g(te), g(tr)), (obs, nobs, act, rew, te, tr)
 
 
-def gae_roofline(device, T=128, N=8192, sets=16, reps=4):
-    """GAE kernel alone over `sets` distinct buffer sets (22 B/elem x 1,048,576 elem x 16 = 369 MB
-    > 256 MB Infinity Cache), launched back to back; each launch's duration comes from the HIP
-    event pair libdppo attaches to the kernel itself (timing mode, hipExtLaunchKernel)."""
+def gae_roofline(device, T=128, N=8192, sets=None, reps=4, mode=0):
+    """GAE kernel alone over distinct buffer sets rotated past the 256 MB Infinity Cache (at
+    N = 8192: 16 sets x 22 B/elem x 1,048,576 elem = 369 MB; at N = 65,536: 2 sets x 184 MB),
+    launched back to back; each launch's duration comes from the HIP event pair libdppo attaches
+    to the kernel itself (timing mode, hipExtLaunchKernel).  mode: 0 = the bit-exact serial scan
+    (the default), 1 = the chunked affine scan (tolerance mode, dppo_set_gae_mode)."""
     from diamond import _native as NN
+    if sets is None:
+        sets = max(2, -(-369 * 2 ** 20 // (22 * T * N)))
+    if N >= 65536:
+        reps = max(reps, 16)
     h = NN.Handle(device.index or 0, NN.Dims(T, N, 1, 1, 0, 64, 1, 1, 1, 0))
+    h.set_gae_mode(mode)
     rng = np.random.default_rng(1)
     bufs = []
     for _ in range(sets):
@@ -138,14 +146,20 @@ def gae_roofline(device, T=128, N=8192, sets=16, reps=4):
     achieved = nbytes / (per * 1e-3) / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = f"gae{N}" + ("_affine" if mode else "")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(f"gae{N}", {}).get("gae")
+            traffic = json.load(open(pmc)).get(key, {}).get("gae")
         except Exception:
             traffic = None
+    h.close()
+    del bufs
+    torch.cuda.empty_cache()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "gae_pipe_kernel<32>", "num_envs": N, "rollout_steps": T,
+            "kernel": "gae_aff_kernel<32>" if mode else "gae_pipe_kernel<32>",
+            "mode": "affine (<= 1e-6 of scale)" if mode else "exact (bit-exact serial)",
+            "num_envs": N, "rollout_steps": T,
             "bytes_per_launch": nbytes, "us_per_launch": round(per * 1e3, 2),
             "launches": cnt, "rotating_sets": sets}
 
@@ -410,6 +424,10 @@ def main():
         out["configs_extra"] = extra
     if rank == 0 and world == 1 and not args.no_gae_roofline:
         out["roofline_gae"] = gae_roofline(device)
+        out["roofline_gae_affine"] = gae_roofline(device, mode=1)
+        # C5's one-GPU buffer (65,536 envs, 184 MB per launch): the launch ramp amortised
+        out["roofline_gae_65536"] = {"exact": gae_roofline(device, N=65536),
+                                     "affine": gae_roofline(device, N=65536, mode=1)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         tb, nb = cpu_baselines(args.config if args.config != "c5" else "cartpole4096")
         out["cpu_baseline"] = tb

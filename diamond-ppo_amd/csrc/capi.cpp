@@ -98,6 +98,7 @@ struct dppo_handle {
   int32_t* perms_local = nullptr;    // [E][B]
   int32_t* seg = nullptr;            // [E][M + 1]
   int32_t* sel_cnt = nullptr;        // [E][shard_select_chunks(Bg)]
+  int gae_mode = DPPO_GAE_EXACT;
   int G = 1;       // workgroups (= gradient slabs) of the fused minibatch kernel
   int num_cus = 256;
   int64_t slab_stride = 0;
@@ -416,7 +417,7 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
     Timed tm(h, K_GAE, s);
     DPPO_TRY(launch_gae(ro->rewards, ro->term, ro->trunc, h->values, h->next_values, h->adv,
                         h->ret, h->partials, d.rollout_steps, d.num_envs, hp->gamma,
-                        hp->gae_lambda, s, &h->n_partials));
+                        hp->gae_lambda, s, &h->n_partials, h->gae_mode));
   }
   // (4) advantage statistics, global over ranks (ppo.py:243)
   if (hp->advantage_norm) {
@@ -895,7 +896,16 @@ int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, cons
   Timed tm(h, K_GAE, S(stream));
   return launch_gae(rewards, term, trunc, values, next_values, adv, returns, h->partials,
                     h->dims.rollout_steps, h->dims.num_envs, gamma, gae_lambda, S(stream),
-                    &h->n_partials);
+                    &h->n_partials, h->gae_mode);
+}
+
+int dppo_set_gae_mode(dppo_handle* h, int32_t mode) {
+  if (!h || (mode != DPPO_GAE_EXACT && mode != DPPO_GAE_AFFINE)) {
+    set_error("invalid argument to dppo_set_gae_mode");
+    return DPPO_EINVAL;
+  }
+  h->gae_mode = mode;
+  return DPPO_OK;
 }
 
 int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream) {

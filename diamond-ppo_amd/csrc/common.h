@@ -76,7 +76,8 @@ __device__ __forceinline__ f32x2 tanh2(f32x2 x) {
 // Launchers implemented in the .hip files (all stream-ordered, no host sync).
 int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
                const float* nv, float* adv, float* ret, double* partials, int T, int N,
-               float gamma, float gae_lambda, hipStream_t s, int* n_partials);
+               float gamma, float gae_lambda, hipStream_t s, int* n_partials,
+               int mode = DPPO_GAE_EXACT);
 int launch_stats_reduce(const double* partials, int n_partials, double* dsum, hipStream_t s);
 int launch_stats_finalize(const double* dsum, double n_total, float* mean_std, hipStream_t s);
 int launch_adv_normalize(float* adv, const float* mean_std, int64_t n, hipStream_t s);

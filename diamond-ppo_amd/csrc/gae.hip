@@ -449,6 +449,151 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
   }
 }
 
+// ---- Affine-scan GAE (tolerance mode, SURVEY §7.2 hard part 1 / §8(c): <= 1e-6 relative) ------
+// The recurrence a_t = delta_t + coef_t * a_{t+1} is an affine map of the carried advantage, and
+// affine maps compose: over a 16-step chunk, a_j = b_j + p_j * a_end with b, p the chunk's local
+// scan from the identity (b = 0, p = 1 at its end).  So every chunk owner scans its own 16 steps
+// at once -- all 8 owners of a 128-step super-chunk in parallel, instead of one wave walking 128
+// dependent steps -- publishes its chunk map (B, P) = (b_0, p_0), and after ONE workgroup barrier
+// folds the maps of the later chunks (<= 7 dependent steps) into its carry and finishes its rows.
+// The chunk that ends the rollout is bit-exact (carry 0); elsewhere the re-association costs a few
+// ulp (the parity test bounds it at 1e-6 of the advantages' scale).  8 waves, one per chunk,
+// no scan wave, no stagger: every load of the tile goes out at once.
+template <int E>
+struct AffLds {
+  float delta[E][kPStride];  // env-major rows of this super-chunk (wave-private row ranges)
+  float coef[E][kPStride];
+  float a[E][kPStride];
+  float B[2][kPChunks][E];   // chunk maps, double-buffered by iteration parity
+  float P[2][kPChunks][E];
+  float carry[2][E];         // advantage at the end of the current super-chunk
+  double wsum[kPChunks][2];
+};
+
+template <int E>
+__global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
+    const float* __restrict__ rew, const uint8_t* __restrict__ term,
+    const uint8_t* __restrict__ trunc, const float* __restrict__ val,
+    const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
+    double* __restrict__ partials, int T, int N, float g, float c) {
+  __shared__ __attribute__((aligned(16))) AffLds<E> L;
+  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;  // wave k owns chunk k
+  const int ntiles = N / E;
+  const int nsup = (T + kPSuper - 1) / kPSuper;
+  constexpr int V4 = E / 4;              // lanes per row (4 envs each)
+  constexpr int RP = kWave / V4;         // rows per pass
+  constexpr int PER = kPChunk / RP;      // passes per chunk
+  const int e0 = 4 * (lane % V4);
+  const int r0 = k * kPChunk;
+  double lsum = 0.0, lsq = 0.0;
+  int it = 0;
+  for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
+    const int n0 = pipe_tile<E>(lb, ntiles) * E;
+    for (int s = 0; s < nsup; ++s, ++it) {
+      const int par = it & 1;
+      const int hi = T - s * kPSuper;
+      const int lo = hi > kPSuper ? hi - kPSuper : 0;
+      const int nr = min(kPChunk, hi - lo - r0);
+      f32x4 xr[PER], xv[PER], xn[PER];
+      uint32_t xt[PER], xu[PER];
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int row = p * RP + lane / V4;
+        if (row < nr) {
+          const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
+          xr[p] = *(const f32x4*)(rew + go);
+          xv[p] = *(const f32x4*)(val + go);
+          xn[p] = *(const f32x4*)(nval + go);
+          xt[p] = *(const uint32_t*)(term + go);
+          xu[p] = *(const uint32_t*)(trunc + go);
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int row = p * RP + lane / V4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = -0.0f, cf = 1.0f;  // rows past the rollout: the identity map
+          if (row < nr)
+            gae_terms(xr[p][j], xv[p][j], xn[p][j], ((xt[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f,
+                      ((xu[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f, g, c, d, cf);
+          L.delta[e0 + j][r0 + row] = d;
+          L.coef[e0 + j][r0 + row] = cf;
+        }
+      }
+      // local scan of the chunk from the identity, lane = env (this wave's own LDS rows: its
+      // LDS operations complete in order)
+      float bl[kPChunk], pl[kPChunk];
+      if (lane < E) {
+        f32x4 d4[4], c4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          d4[q] = *(const f32x4*)&L.delta[lane][r0 + 4 * q];
+          c4[q] = *(const f32x4*)&L.coef[lane][r0 + 4 * q];
+        }
+        float b = 0.0f, pp = 1.0f;
+#pragma unroll
+        for (int j = kPChunk - 1; j >= 0; --j) {
+          b = gae_carry(d4[j >> 2][j & 3], c4[j >> 2][j & 3], b);
+          pp = c4[j >> 2][j & 3] * pp;
+          bl[j] = b;
+          pl[j] = pp;
+        }
+        L.B[par][k][lane] = bl[0];
+        L.P[par][k][lane] = pl[0];
+      }
+      __syncthreads();
+      if (lane < E) {
+        // the carry into this chunk: the later super-chunk's, then the later chunks' maps
+        float cin = s == 0 ? 0.0f : L.carry[par][lane];
+        for (int j = kPChunks - 1; j > k; --j) cin = gae_carry(L.B[par][j][lane], L.P[par][j][lane], cin);
+        f32x4 av[4];
+#pragma unroll
+        for (int j = 0; j < kPChunk; ++j) av[j >> 2][j & 3] = gae_carry(bl[j], pl[j], cin);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[lane][r0 + 4 * q] = av[q];
+        if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
+      }
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const int row = p * RP + lane / V4;
+        if (row < nr) {
+          const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
+          f32x4 av;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
+          *(f32x4*)(adv + go) = av;
+          *(f32x4*)(ret + go) = xv[p] + av;  // returns = values + advantages (ppo.py:241)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            lsum += (double)av[j];
+            lsq += (double)av[j] * (double)av[j];
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    lsum += __shfl_xor(lsum, off);
+    lsq += __shfl_xor(lsq, off);
+  }
+  if (lane == 0) {
+    L.wsum[k][0] = lsum;
+    L.wsum[k][1] = lsq;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int j = 0; j < kPChunks; ++j) {
+      s0 += L.wsum[j][0];
+      s1 += L.wsum[j][1];
+    }
+    partials[2 * blockIdx.x] = s0;
+    partials[2 * blockIdx.x + 1] = s1;
+  }
+}
+
 // Sum the per-tile partials in a fixed order: dsum = {sum, sumsq}.
 __global__ __launch_bounds__(256) void stats_reduce_kernel(const double* __restrict__ partials,
                                                            int n, double* __restrict__ dsum) {
@@ -570,7 +715,7 @@ extern "C" __attribute__((visibility("default"))) int dppo_debug_gae_trace(long 
 
 int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
                const float* nv, float* adv, float* ret, double* partials, int T, int N,
-               float gamma, float gae_lambda, hipStream_t s, int* n_partials) {
+               float gamma, float gae_lambda, hipStream_t s, int* n_partials, int mode) {
   const int G = (N + kEnvTile - 1) / kEnvTile;
   *n_partials = G;
   if (T <= 0 || N <= 0) return DPPO_OK;
@@ -607,7 +752,14 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
     if (!e32 && grid >= 16) grid -= grid % 16;
     *n_partials = grid;
-    if (e32)
+    if (mode == DPPO_GAE_AFFINE) {
+      if (e32)
+        DPPO_LAUNCH(gae_aff_kernel<32>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
+                    nv, adv, ret, partials, T, N, gamma, c);
+      else
+        DPPO_LAUNCH(gae_aff_kernel<16>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
+                    nv, adv, ret, partials, T, N, gamma, c);
+    } else if (e32)
       DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
                   adv, ret, partials, T, N, gamma, c, wt, stagger);
     else

@@ -20,12 +20,13 @@ DPPO_EUNSUPPORTED = -3
 DPPO_ENOMEM = -4
 DPPO_ECOMM = -5
 MAX_TENSORS = 16
+GAE_EXACT, GAE_AFFINE = 0, 1  # dppo_set_gae_mode
 TRACE_FIELDS = 5
 PERM_SLOTS = 3  # pinned permutation staging slots per handle (include/dppo.h DPPO_PERM_SLOTS)
 
 EXPORTED = [
     "dppo_version", "dppo_last_error", "dppo_param_layout", "dppo_create", "dppo_destroy",
-    "dppo_gae_f32", "dppo_adv_stats", "dppo_adv_sums", "dppo_adv_stats_from_sums",
+    "dppo_gae_f32", "dppo_set_gae_mode", "dppo_adv_stats", "dppo_adv_sums", "dppo_adv_stats_from_sums",
     "dppo_adv_normalize_f32", "dppo_old_policy_f32",
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
@@ -96,6 +97,7 @@ def load():
         "dppo_destroy": (None, [vp]),
         "dppo_gae_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
         "dppo_adv_stats": (ctypes.c_int, [vp, vp, vp]),
+        "dppo_set_gae_mode": (ctypes.c_int, [vp, i32]),
         "dppo_adv_normalize_f32": (ctypes.c_int, [vp, vp, i64, vp]),
         "dppo_adv_sums": (ctypes.c_int, [vp, vp, vp]),
         "dppo_adv_stats_from_sums": (ctypes.c_int, [vp, f64, vp, vp]),
@@ -282,6 +284,9 @@ class Handle:
         out = np.zeros((rows, TRACE_FIELDS), np.float32)
         check(self.lib.dppo_get_trace(self.h, out.ctypes.data, int(rows)), "dppo_get_trace")
         return out
+
+    def set_gae_mode(self, mode: int):
+        check(self.lib.dppo_set_gae_mode(self.h, int(mode)), "dppo_set_gae_mode")
 
     def set_timing(self, enable: bool):
         check(self.lib.dppo_set_timing(self.h, int(bool(enable))), "dppo_set_timing")

@@ -58,6 +58,9 @@ class ContinuousPPOConfig:
     # the reference's permutations of the GLOBAL batch (ppo.py:252-255) and processes its members
     # of each global minibatch, so N ranks reproduce the single-GPU learn() of the global batch
     global_minibatches: bool = False
+    # GAE kernel (additive): True = the reference's serial recurrence, bit-exact; False = the
+    # chunked affine scan (chunk maps composed in parallel), within 1e-6 of the advantages' scale
+    gae_bitexact: bool = True
     tanh_squash: bool = False  # extension: env actions tanh(u), experience keeps u (module doc)
 
 

@@ -344,6 +344,8 @@ class NativeLearner:
                            rank=self.rank, global_minibatches=int(self.global_mb))
         self.perm_n = self.T * self.N * (self.world if self.global_mb else 1)
         self.handle = N.Handle(device.index or 0, self.dims)
+        if not getattr(cfg, "gae_bitexact", True):
+            self.handle.set_gae_mode(N.GAE_AFFINE)
         L = self.handle.layout
         names = [n for n, _ in network.named_parameters()]
         shapes_ok = network_is_default and L.count == len(names) and all(

@@ -55,6 +55,9 @@ class PPOConfig:
     # the reference's permutations of the GLOBAL batch (ppo.py:252-255) and processes its members
     # of each global minibatch, so N ranks reproduce the single-GPU learn() of the global batch
     global_minibatches: bool = False
+    # GAE kernel (additive): True = the reference's serial recurrence, bit-exact; False = the
+    # chunked affine scan (chunk maps composed in parallel), within 1e-6 of the advantages' scale
+    gae_bitexact: bool = True
 
 
 class ActorCriticNetwork(nn.Module):
@@ -253,6 +256,8 @@ class _AgentBase:
             d = N.Dims(rollout_steps=T, num_envs=Nn, obs_dim=1, act_dim=1, continuous=0,
                        hidden=64, num_epochs=1, num_minibatches=1, world_size=1, rank=0)
             cache[key] = N.Handle(self.device.index or 0, d)
+            if not getattr(self.cfg, "gae_bitexact", True):
+                cache[key].set_gae_mode(N.GAE_AFFINE)
         return cache[key]
 
     def learn(self, experience: list[list[np.ndarray]]) -> None:

@@ -59,6 +59,7 @@ class RecurrentPPOConfig:
     save_interval: float = 600
     verbose: bool = True
     device_index: int = 0
+    gae_bitexact: bool = True   # False: the chunked affine-scan GAE kernel (PPOConfig)
 
 
 class GRUCore(nn.GRU):
@@ -142,6 +143,8 @@ class RecurrentPPO:
                       num_epochs=cfg.num_epochs, num_minibatches=cfg.num_minibatches,
                       world_size=1, rank=0)
         self.handle = N.Handle(self.device.index or 0, dims)
+        if not getattr(cfg, "gae_bitexact", True):
+            self.handle.set_gae_mode(N.GAE_AFFINE)
         if world > 1:   # replicate rank 0's initial weights (identical seeds: a no-op in practice)
             d = torch.distributed
             if d.get_backend() == "nccl":

@@ -39,6 +39,11 @@ extern "C" {
 #define DPPO_ENOMEM (-4)       /* workspace allocation failed (Python: MemoryError) */
 #define DPPO_ECOMM (-5)        /* RCCL failure (Python: RuntimeError) */
 
+/* GAE modes (dppo_set_gae_mode): the reference's serial recurrence, bit-exact (default); or the
+ * chunked affine scan, within 1e-6 of the advantages' scale (SURVEY 7.2 hard part 1). */
+#define DPPO_GAE_EXACT 0
+#define DPPO_GAE_AFFINE 1
+
 #define DPPO_MAX_TENSORS 16
 #define DPPO_TRACE_FIELDS 5 /* per optimizer step: loss, loss_policy, loss_value, entropy, grad_norm */
 
@@ -126,6 +131,11 @@ void dppo_destroy(dppo_handle* h);
 int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, const uint8_t* trunc,
                  const float* values, const float* next_values, float* adv, float* returns,
                  float gamma, float gae_lambda, void* stream);
+
+/* Select the GAE kernel of this handle's dppo_gae_f32 / dppo_learn_f32 calls: DPPO_GAE_EXACT
+ * (default; bit-exact with ppo.py:197-220) or DPPO_GAE_AFFINE (chunk maps composed in parallel;
+ * re-associated fp32, <= 1e-6 of the advantages' scale from the reference). */
+int dppo_set_gae_mode(dppo_handle* h, int32_t mode);
 
 /* Mean and unbiased std of the advantages of the last dppo_gae_f32 (ppo.py:243, reduced over
  * all ranks when a communicator is attached); writes device float mean_std[2]. */

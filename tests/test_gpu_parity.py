@@ -42,9 +42,10 @@ def gae_handle(T, Nn):
 
 
 # ---------------------------------------------------------------------------------------------
-def run_gae(r, te, tr, v, nv):
+def run_gae(r, te, tr, v, nv, mode=0):
     T, Nn = r.shape
     h = gae_handle(T, Nn)
+    h.set_gae_mode(mode)
     adv = torch.empty(T, Nn, device=dev())
     ret = torch.empty(T, Nn, device=dev())
     ms = torch.zeros(4, device=dev())
@@ -90,6 +91,56 @@ def test_gae_vs_oracle_sizes(T, Nn):
         mean, std = P.adv_stats(ref)
         assert abs(ms[0] - mean) <= 1e-6 * max(1.0, abs(mean))
         assert abs(ms[1] - std) <= 2e-6 * std
+
+
+@pytest.mark.parametrize("T,Nn", [(128, 8192), (128, 65536), (128, 4096), (300, 64),
+                                  (129, 4096), (200, 8448), (64, 6144), (16, 12288), (1, 32),
+                                  (100, 512), (7, 4104)])
+def test_gae_affine_mode_within_tolerance(T, Nn):
+    """DPPO_GAE_AFFINE (SURVEY §7.2 / §8(c) tolerance mode): every chunk's affine map composed in
+    parallel.  Against the bit-exact oracle: |adv - ref| <= 1e-6 x max|ref| (and returns the
+    same), statistics rel 1e-6; T > 128 chains super-chunks, T % 16 != 0 and T < 16 leave
+    identity rows, N % 32 != 0 runs the 16-env tiles (N % 16 != 0: the serial kernel)."""
+    from oracle import ppo_np as P
+    rng = np.random.default_rng(T * 17 + Nn)
+    r = rng.normal(1, 1, (T, Nn)).astype(np.float32)
+    te = (rng.random((T, Nn)) < 0.02).astype(np.uint8)
+    tr = (rng.random((T, Nn)) < 0.005).astype(np.uint8)
+    v = rng.standard_normal((T, Nn)).astype(np.float32)
+    nv = rng.standard_normal((T, Nn)).astype(np.float32)
+    adv, ret, ms, _ = run_gae(r, te, tr, v, nv, mode=N.GAE_AFFINE)
+    ref = P.gae(r, te, tr, v, nv)
+    scale = float(np.abs(ref).max())
+    err = np.abs(adv.astype(np.float64) - ref).max()
+    assert err <= 1e-6 * scale, (err, scale)
+    assert np.abs(ret.astype(np.float64) - (v + ref)).max() <= 1e-6 * scale + 1e-6
+    if T % 16 == 0:  # the rollout's last 16 steps start from carry 0: bit-exact
+        assert np.array_equal(adv[-16:], ref[-16:])
+    mean, std = P.adv_stats(ref)
+    assert abs(ms[0] - mean) <= 1e-6 * max(1.0, abs(mean))
+    assert abs(ms[1] - std) <= 2e-6 * std
+
+
+@pytest.mark.parametrize("name", ["lunar_medium", "cheetah_small", "cartpole_c1"])
+def test_learn_with_affine_gae_matches_reference_trace(name):
+    """learn() with the tolerance-mode GAE (cfg.gae_bitexact = False) stays within the golden
+    traces' tolerances (advantages 5e-5, losses / norms rel 2e-5, parameters 5e-6)."""
+    z = load_golden(f"learn_{name}.npz")
+    T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
+    agent = make_agent(z)
+    agent._learner.handle.set_gae_mode(N.GAE_AFFINE)
+    losses = []
+    for li in range(n_learn):
+        np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
+                             int(z[f"rng_pos_before{li}"]), 0, 0.0))
+        ro = diamond.engine.stage_experience(experience(z, li), dev(), bool(cont))
+        agent.learn_device(ro)
+        losses += list(agent.learn_trace()[:, 0])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(losses, z["loss"], rtol=2e-5, atol=2e-5)
+    for n, p in agent.network.named_parameters():
+        np.testing.assert_allclose(p.detach().cpu().numpy(), z["final/" + n], rtol=0, atol=5e-6,
+                                   err_msg=n)
 
 
 def test_gae_full_size_properties():
