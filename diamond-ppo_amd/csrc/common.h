@@ -285,6 +285,22 @@ struct RankPtrs {
 int launch_rank_sum(const RankPtrs& src, int n, void* out, int64_t count, bool f64,
                     hipStream_t s);
 
+// RecurrentPPO fused minibatch gradient (gru.hip): parameter offsets in the flat layout
+// (RecurrentActorCriticNetwork.named_parameters() order) and the per-sample scratch arrays.
+struct GruOffsets {
+  int64_t Wb, bb, Wih, Whh, bih, bhh, Wa1, ba1, Wa2, ba2, Wc1, bc1, Wc2, bc2;
+};
+struct GruScratch {
+  float *obs, *x1, *gi, *hi, *ho, *r, *z, *n, *ghn, *ya, *yc, *dl, *dv, *dya, *dyc, *dho, *dgi,
+      *dgh, *dx1;
+};
+size_t gru_lds_bytes(int D);
+int gru_grid(int N);
+int launch_gru_grad(const GruOffsets& po, const float* params, const dppo_gru_batch& b,
+                    const int32_t* idx, int32_t m, float* wmask, int64_t B, int T, int N, int D,
+                    int A, float inv_m, float clip_eps, float vf, float ent, const GruScratch& sc,
+                    float* slabs, int64_t slab_stride, int64_t p_total, hipStream_t s);
+
 // Fisher-Yates resolution (shuffle.hip): perms[c][n] from swap targets[c][n];
 // scratch = 3 * count * n int32.
 int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,

@@ -485,93 +485,114 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
   constexpr int PER = kPChunk / RP;      // passes per chunk
   const int e0 = 4 * (lane % V4);
   const int r0 = k * kPChunk;
-  double lsum = 0.0, lsq = 0.0;
-  int it = 0;
-  for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
-    const int n0 = pipe_tile<E>(lb, ntiles) * E;
-    for (int s = 0; s < nsup; ++s, ++it) {
-      const int par = it & 1;
-      const int hi = T - s * kPSuper;
-      const int lo = hi > kPSuper ? hi - kPSuper : 0;
-      const int nr = min(kPChunk, hi - lo - r0);
-      f32x4 xr[PER], xv[PER], xn[PER];
-      uint32_t xt[PER], xu[PER];
+  // iterations q = (tile, super-chunk) pairs of this workgroup, super-chunks latest first
+  const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int niter = my_tiles * nsup;
+  struct Ops {
+    f32x4 r[PER], v[PER], nv[PER];
+    uint32_t te[PER], tr[PER];
+  };
+  auto geom = [&](int q, int64_t& base, int& lo, int& nr, int& s) {
+    const int lb = blockIdx.x + (q / nsup) * gridDim.x;
+    s = q % nsup;
+    const int hi = T - s * kPSuper;
+    lo = hi > kPSuper ? hi - kPSuper : 0;
+    nr = min(kPChunk, hi - lo - r0);
+    base = (int64_t)(lo + r0) * N + pipe_tile<E>(lb, ntiles) * E + e0;
+  };
+  auto load = [&](int q, Ops& o) {
+    int64_t base;
+    int lo, nr, s;
+    geom(q, base, lo, nr, s);
 #pragma unroll
-      for (int p = 0; p < PER; ++p) {
-        const int row = p * RP + lane / V4;
-        if (row < nr) {
-          const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
-          xr[p] = *(const f32x4*)(rew + go);
-          xv[p] = *(const f32x4*)(val + go);
-          xn[p] = *(const f32x4*)(nval + go);
-          xt[p] = *(const uint32_t*)(term + go);
-          xu[p] = *(const uint32_t*)(trunc + go);
-        }
+    for (int p = 0; p < PER; ++p) {
+      const int row = p * RP + lane / V4;
+      if (row < nr) {
+        const int64_t go = base + (int64_t)row * N;
+        o.r[p] = *(const f32x4*)(rew + go);
+        o.v[p] = *(const f32x4*)(val + go);
+        o.nv[p] = *(const f32x4*)(nval + go);
+        o.te[p] = *(const uint32_t*)(term + go);
+        o.tr[p] = *(const uint32_t*)(trunc + go);
       }
+    }
+  };
+  double lsum = 0.0, lsq = 0.0;
+  Ops cur{}, nxt{};
+  if (niter > 0) load(0, cur);
+  for (int q = 0; q < niter; ++q) {
+    const int par = q & 1;
+    int64_t base;
+    int lo, nr, s;
+    geom(q, base, lo, nr, s);
 #pragma unroll
-      for (int p = 0; p < PER; ++p) {
-        const int row = p * RP + lane / V4;
+    for (int p = 0; p < PER; ++p) {
+      const int row = p * RP + lane / V4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float d = -0.0f, cf = 1.0f;  // rows past the rollout: the identity map
+        if (row < nr)
+          gae_terms(cur.r[p][j], cur.v[p][j], cur.nv[p][j],
+                    ((cur.te[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f,
+                    ((cur.tr[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f, g, c, d, cf);
+        L.delta[e0 + j][r0 + row] = d;
+        L.coef[e0 + j][r0 + row] = cf;
+      }
+    }
+    // the next iteration's operands go out now: they land while this one is scanned and stored
+    if (q + 1 < niter) load(q + 1, nxt);
+    // local scan of the chunk from the identity, lane = env (this wave's own LDS rows: its LDS
+    // operations complete in order)
+    float bl[kPChunk], pl[kPChunk];
+    if (lane < E) {
+      f32x4 d4[4], c4[4];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        d4[qq] = *(const f32x4*)&L.delta[lane][r0 + 4 * qq];
+        c4[qq] = *(const f32x4*)&L.coef[lane][r0 + 4 * qq];
+      }
+      float b = 0.0f, pp = 1.0f;
+#pragma unroll
+      for (int j = kPChunk - 1; j >= 0; --j) {
+        b = gae_carry(d4[j >> 2][j & 3], c4[j >> 2][j & 3], b);
+        pp = c4[j >> 2][j & 3] * pp;
+        bl[j] = b;
+        pl[j] = pp;
+      }
+      L.B[par][k][lane] = bl[0];
+      L.P[par][k][lane] = pl[0];
+    }
+    __syncthreads();
+    if (lane < E) {
+      // the carry into this chunk: the later super-chunk's, then the later chunks' maps
+      float cin = s == 0 ? 0.0f : L.carry[par][lane];
+      for (int j = kPChunks - 1; j > k; --j)
+        cin = gae_carry(L.B[par][j][lane], L.P[par][j][lane], cin);
+      f32x4 av[4];
+#pragma unroll
+      for (int j = 0; j < kPChunk; ++j) av[j >> 2][j & 3] = gae_carry(bl[j], pl[j], cin);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) *(f32x4*)&L.a[lane][r0 + 4 * qq] = av[qq];
+      if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
+    }
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      const int row = p * RP + lane / V4;
+      if (row < nr) {
+        const int64_t go = base + (int64_t)row * N;
+        f32x4 av;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
+        *(f32x4*)(adv + go) = av;
+        *(f32x4*)(ret + go) = cur.v[p] + av;  // returns = values + advantages (ppo.py:241)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float d = -0.0f, cf = 1.0f;  // rows past the rollout: the identity map
-          if (row < nr)
-            gae_terms(xr[p][j], xv[p][j], xn[p][j], ((xt[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f,
-                      ((xu[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f, g, c, d, cf);
-          L.delta[e0 + j][r0 + row] = d;
-          L.coef[e0 + j][r0 + row] = cf;
-        }
-      }
-      // local scan of the chunk from the identity, lane = env (this wave's own LDS rows: its
-      // LDS operations complete in order)
-      float bl[kPChunk], pl[kPChunk];
-      if (lane < E) {
-        f32x4 d4[4], c4[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          d4[q] = *(const f32x4*)&L.delta[lane][r0 + 4 * q];
-          c4[q] = *(const f32x4*)&L.coef[lane][r0 + 4 * q];
-        }
-        float b = 0.0f, pp = 1.0f;
-#pragma unroll
-        for (int j = kPChunk - 1; j >= 0; --j) {
-          b = gae_carry(d4[j >> 2][j & 3], c4[j >> 2][j & 3], b);
-          pp = c4[j >> 2][j & 3] * pp;
-          bl[j] = b;
-          pl[j] = pp;
-        }
-        L.B[par][k][lane] = bl[0];
-        L.P[par][k][lane] = pl[0];
-      }
-      __syncthreads();
-      if (lane < E) {
-        // the carry into this chunk: the later super-chunk's, then the later chunks' maps
-        float cin = s == 0 ? 0.0f : L.carry[par][lane];
-        for (int j = kPChunks - 1; j > k; --j) cin = gae_carry(L.B[par][j][lane], L.P[par][j][lane], cin);
-        f32x4 av[4];
-#pragma unroll
-        for (int j = 0; j < kPChunk; ++j) av[j >> 2][j & 3] = gae_carry(bl[j], pl[j], cin);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[lane][r0 + 4 * q] = av[q];
-        if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
-      }
-#pragma unroll
-      for (int p = 0; p < PER; ++p) {
-        const int row = p * RP + lane / V4;
-        if (row < nr) {
-          const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
-          f32x4 av;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
-          *(f32x4*)(adv + go) = av;
-          *(f32x4*)(ret + go) = xv[p] + av;  // returns = values + advantages (ppo.py:241)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            lsum += (double)av[j];
-            lsq += (double)av[j] * (double)av[j];
-          }
+          lsum += (double)av[j];
+          lsq += (double)av[j] * (double)av[j];
         }
       }
     }
+    cur = nxt;
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {

@@ -33,6 +33,7 @@ EXPORTED = [
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
     "dppo_perm_targets_numpy", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
+    "dppo_gru_param_layout", "dppo_gru_create", "dppo_gru_destroy", "dppo_gru_minibatch_grad_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
                   "allreduce", "perm", "reduce_adam"]
@@ -61,6 +62,19 @@ class Layout(ctypes.Structure):
                 ("count", ctypes.c_int32), ("pad_", ctypes.c_int32),
                 ("offset", ctypes.c_int64 * MAX_TENSORS), ("numel", ctypes.c_int64 * MAX_TENSORS),
                 ("rows", ctypes.c_int32 * MAX_TENSORS), ("cols", ctypes.c_int32 * MAX_TENSORS)]
+
+
+class GruDims(ctypes.Structure):
+    _fields_ = [("rollout_steps", ctypes.c_int32), ("num_envs", ctypes.c_int32),
+                ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32),
+                ("hidden", ctypes.c_int32), ("gru_hidden", ctypes.c_int32)]
+
+
+class GruBatch(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_void_p), ("actions", ctypes.c_void_p),
+                ("old_log_probs", ctypes.c_void_p), ("advantages", ctypes.c_void_p),
+                ("returns", ctypes.c_void_p), ("prev_dones", ctypes.c_void_p),
+                ("hx0", ctypes.c_void_p)]
 
 
 class Rollout(ctypes.Structure):
@@ -127,6 +141,11 @@ def load():
         "dppo_status": (ctypes.c_int, [vp]),
         "dppo_actor_forward_f32": (ctypes.c_int, [vp, vp, vp, i64, vp, vp]),
         "dppo_fanin_selftest": (ctypes.c_int, [vp, i32, i32, i64, vp]),
+        "dppo_gru_param_layout": (ctypes.c_int, [P(GruDims), P(Layout)]),
+        "dppo_gru_create": (ctypes.c_int, [ctypes.c_int, P(GruDims), P(vp)]),
+        "dppo_gru_destroy": (None, [vp]),
+        "dppo_gru_minibatch_grad_f32": (ctypes.c_int, [vp, vp, P(GruBatch), vp, i32, i32,
+                                                       P(HParams), vp, vp]),
         "dppo_set_timing": (ctypes.c_int, [vp, i32]),
         "dppo_get_timing": (ctypes.c_int, [vp, vp, vp]),
     }
@@ -301,6 +320,32 @@ class Handle:
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         buf = ctypes.create_string_buffer(uid, 128)
         check(self.lib.dppo_comm_init(self.h, int(nranks), int(rank), buf), "dppo_comm_init")
+
+
+class GruHandle:
+    """Owns one dppo_gru_handle (RecurrentPPO's fused minibatch-gradient workspace)."""
+
+    def __init__(self, device_index: int, dims: GruDims):
+        self.lib = load()
+        self.dims = dims
+        h = ctypes.c_void_p()
+        check(self.lib.dppo_gru_create(int(device_index), ctypes.byref(dims), ctypes.byref(h)),
+              "dppo_gru_create")
+        self.h = h
+        self.layout = Layout()
+        check(self.lib.dppo_gru_param_layout(ctypes.byref(dims), ctypes.byref(self.layout)),
+              "dppo_gru_param_layout")
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.lib.dppo_gru_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def loopback_group(handles) -> None:

@@ -18,6 +18,7 @@ is its local mean scaled by 1/world, and the flat gradient is all-reduced (SUM, 
 """
 from __future__ import annotations
 
+import ctypes
 import time
 from dataclasses import dataclass
 from math import sqrt
@@ -119,6 +120,11 @@ def network_parameter_init_(network: nn.Module, gain: float = 1.0) -> None:
 
 
 class RecurrentPPO:
+    # learn() runs each minibatch's sequence recompute, loss and BPTT as one fused HIP launch
+    # (dppo_gru_minibatch_grad_f32) for the default network at supported shapes; False (or any
+    # other network_cls) runs the network under torch autograd on the GPU
+    fused_gru = True
+
     def __init__(self, env_fn: Callable[[], Any], cfg: RecurrentPPOConfig = RecurrentPPOConfig(),
                  network_cls: Any = RecurrentActorCriticNetwork, envs=None) -> None:
         self.device = require_gpu(cfg.device_index)
@@ -143,6 +149,18 @@ class RecurrentPPO:
                       num_epochs=cfg.num_epochs, num_minibatches=cfg.num_minibatches,
                       world_size=1, rank=0)
         self.handle = N.Handle(self.device.index or 0, dims)
+        self.gru = None
+        obs_dim = int(np.prod(obs_space.shape))
+        if (type(self.network) is RecurrentActorCriticNetwork and cfg.network_hidden_dim == 64
+                and cfg.gru_hidden_dim == 16 and obs_dim <= 32 and int(act_space.n) <= 16):
+            gd = N.GruDims(rollout_steps=cfg.rollout_steps, num_envs=cfg.num_envs,
+                           obs_dim=obs_dim, act_dim=int(act_space.n), hidden=64, gru_hidden=16)
+            self.gru = N.GruHandle(self.device.index or 0, gd)
+            L = self.gru.layout
+            if L.total != self.flat.total or any(L.offset[i] != o for i, o in
+                                                  enumerate(self.flat.offsets)):
+                raise RuntimeError("RecurrentActorCriticNetwork layout differs from libdppo's")
+        self.last_losses = None
         if not getattr(cfg, "gae_bitexact", True):
             self.handle.set_gae_mode(N.GAE_AFFINE)
         if world > 1:   # replicate rank 0's initial weights (identical seeds: a no-op in practice)
@@ -245,6 +263,12 @@ class RecurrentPPO:
             cfg.num_epochs, cfg.num_minibatches, mb)
         step = adam_step_count(self.optimizer, self.flat)
         lr = self.optimizer.param_groups[0]["lr"]
+        if self.fused_gru and self.gru is not None:
+            self._learn_fused(observations, actions, log_probs, advantages, returns, prev_dones,
+                              hx, idx, step, lr, world, stream)
+            advance_adam_steps(self.optimizer, self.flat, cfg.num_epochs * cfg.num_minibatches)
+            self.lr_scheduler.step()
+            return
         for b_idx in idx:
             for mb_idx in b_idx:
                 self.flat.grad.zero_()
@@ -270,6 +294,50 @@ class RecurrentPPO:
                     cfg.adam_eps, step, None, stream), "dppo_clip_adam_f32")
         advance_adam_steps(self.optimizer, self.flat, cfg.num_epochs * cfg.num_minibatches)
         self.lr_scheduler.step()
+
+    def _learn_fused(self, observations, actions, log_probs, advantages, returns, prev_dones,
+                     hx, idx, step, lr, world, stream):
+        """Every minibatch: one dppo_gru_minibatch_grad_f32 launch (sequence recompute from hx,
+        loss on the minibatch, BPTT; recurrent_ppo.py:335-360) -> [all-reduce] -> clip + Adam."""
+        cfg, lib = self.cfg, self.gru.lib
+        f32 = lambda x: x.to(torch.float32).contiguous()
+        obs = f32(observations)
+        act = actions.to(torch.int32).contiguous()
+        old_lp, adv, ret = f32(log_probs), f32(advantages), f32(returns)
+        dones = prev_dones.to(torch.uint8).contiguous()
+        hx0 = f32(hx.reshape(cfg.num_envs, cfg.gru_hidden_dim))
+        batch = N.GruBatch(obs.data_ptr(), act.data_ptr(), old_lp.data_ptr(), adv.data_ptr(),
+                           ret.data_ptr(), dones.data_ptr(), hx0.data_ptr())
+        hp = N.HParams(gamma=cfg.gamma, gae_lambda=cfg.gae_lambda, ppo_clip=cfg.ppo_clip,
+                       value_loss_weight=cfg.value_loss_weight, entropy_beta=cfg.entropy_beta,
+                       grad_norm_clip=cfg.grad_norm_clip, adam_beta1=0.9, adam_beta2=0.999,
+                       adam_eps=cfg.adam_eps, advantage_norm=int(bool(cfg.advantage_norm)),
+                       lr=float(lr), adam_step=int(step))
+        idx32 = idx.to(torch.int32).contiguous()
+        mb = idx32.shape[-1]
+        m_total = mb * world          # the union minibatch's size under data parallelism
+        total = self.flat.total
+        losses = []
+        for e in range(idx32.shape[0]):
+            for j in range(idx32.shape[1]):
+                mb_idx = idx32[e, j]
+                N.check(lib.dppo_gru_minibatch_grad_f32(
+                    self.gru.h, self.flat.flat.data_ptr(), ctypes.byref(batch), mb_idx.data_ptr(),
+                    mb, m_total, ctypes.byref(hp), self.flat.grad.data_ptr(), stream),
+                    "dppo_gru_minibatch_grad_f32")
+                if world > 1:
+                    torch.distributed.all_reduce(self.flat.grad)
+                losses.append(self.flat.grad[total:total + 3].clone())
+                step += 1
+                N.check(lib.dppo_clip_adam_f32(
+                    self.flat.flat.data_ptr(), self.flat.grad.data_ptr(), self.m.data_ptr(),
+                    self.v.data_ptr(), total, cfg.grad_norm_clip, float(lr), 0.9, 0.999,
+                    cfg.adam_eps, step, None, stream), "dppo_clip_adam_f32")
+        # {loss, policy, value, entropy} per minibatch (reference never logs these; for tests)
+        sums = torch.stack(losses) / float(m_total)
+        self.last_losses = torch.stack([sums[:, 0] + cfg.value_loss_weight * sums[:, 1]
+                                        - cfg.entropy_beta * sums[:, 2], sums[:, 0], sums[:, 1],
+                                        sums[:, 2]], dim=1)
 
     def train(self) -> None:
         world, rank = dist_world()   # per-rank env seeds, rank-0 checkpoints (as PPO.train)

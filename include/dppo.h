@@ -305,6 +305,47 @@ int dppo_fanin_selftest(dppo_handle* h, int32_t blocks, int32_t lds_bytes, int64
  * gradient + loss partials), summed in rank order on the device.  Not for production use. */
 int dppo_loopback_group(dppo_handle** hs, int32_t n);
 
+/* ---- RecurrentPPO (reference diamond/recurrent_ppo.py; the reference crashes at :78, these
+ * follow its intended semantics: GRU with per-step hidden resets :82-87, the full [T, N] sequence
+ * recomputed from the stored initial hidden state for every minibatch :337-341). */
+typedef struct dppo_gru_handle dppo_gru_handle;
+
+typedef struct dppo_gru_dims {
+  int32_t rollout_steps; /* T */
+  int32_t num_envs;      /* N */
+  int32_t obs_dim;       /* D <= 32 */
+  int32_t act_dim;       /* discrete actions A <= 16 */
+  int32_t hidden;        /* network_hidden_dim, must be 64 */
+  int32_t gru_hidden;    /* gru_hidden_dim, must be 16 */
+} dppo_gru_dims;
+
+/* One rollout as RecurrentPPO.learn stacks it (recurrent_ppo.py:306-316), device pointers. */
+typedef struct dppo_gru_batch {
+  const float* obs;           /* [T][N][D] */
+  const int32_t* actions;     /* [T][N] */
+  const float* old_log_probs; /* [T][N] cached during rollout (:219-232) */
+  const float* advantages;    /* [T][N] (normalised when advantage_norm) */
+  const float* returns;       /* [T][N] */
+  const uint8_t* prev_dones;  /* [T][N] hidden reset before step t where set (:84) */
+  const float* hx0;           /* [N][gru_hidden] hidden state at the rollout's start (:313) */
+} dppo_gru_batch;
+
+/* Flat parameter layout of RecurrentActorCriticNetwork (named_parameters() order, 16-float
+ * aligned offsets; 14 tensors). */
+int dppo_gru_param_layout(const dppo_gru_dims* dims, dppo_layout* out);
+int dppo_gru_create(int device, const dppo_gru_dims* dims, dppo_gru_handle** out);
+void dppo_gru_destroy(dppo_gru_handle* h);
+
+/* One minibatch gradient of the recurrent PPO loss (recurrent_ppo.py:335-360): the GRU sequence
+ * over all T x N samples from hx0, the clipped-surrogate + value + entropy loss on the m samples
+ * idx[0..m) (flat t * N + n), divided by m_total (the global minibatch size), and the analytic
+ * backward through time.  grad [layout.total + 8]: the summed gradient in the flat layout, then
+ * the loss sums {policy, value, entropy} (divide by m_total).  Stream-ordered, deterministic. */
+int dppo_gru_minibatch_grad_f32(dppo_gru_handle* h, const float* params,
+                                const dppo_gru_batch* batch, const int32_t* idx, int32_t m,
+                                int32_t m_total, const dppo_hparams* hp, float* grad,
+                                void* stream);
+
 #pragma GCC visibility pop
 
 #ifdef __cplusplus
