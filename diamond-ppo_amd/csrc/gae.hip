@@ -518,6 +518,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
     }
   };
   double lsum = 0.0, lsq = 0.0;
+  GAE_STAMP(0);
   Ops cur{}, nxt{};
   if (niter > 0) load(0, cur);
   for (int q = 0; q < niter; ++q) {
@@ -539,6 +540,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
         L.coef[e0 + j][r0 + row] = cf;
       }
     }
+    GAE_STAMP(1 + k);
     // the next iteration's operands go out now: they land while this one is scanned and stored
     if (q + 1 < niter) load(q + 1, nxt);
     // local scan of the chunk from the identity, lane = env (this wave's own LDS rows: its LDS
@@ -562,7 +564,9 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
       L.B[par][k][lane] = bl[0];
       L.P[par][k][lane] = pl[0];
     }
+    GAE_STAMP(9 + k);
     __syncthreads();
+    GAE_STAMP(25 + k);
     if (lane < E) {
       // the carry into this chunk: the later super-chunk's, then the later chunks' maps
       float cin = s == 0 ? 0.0f : L.carry[par][lane];
@@ -575,6 +579,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
       for (int qq = 0; qq < 4; ++qq) *(f32x4*)&L.a[lane][r0 + 4 * qq] = av[qq];
       if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
     }
+    GAE_STAMP(33 + k);
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
       const int row = p * RP + lane / V4;
@@ -592,6 +597,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
         }
       }
     }
+    GAE_STAMP(17 + k);
     cur = nxt;
   }
 #pragma unroll
@@ -604,6 +610,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
     L.wsum[k][1] = lsq;
   }
   __syncthreads();
+  GAE_STAMP(41);
   if (threadIdx.x == 0) {
     double s0 = 0.0, s1 = 0.0;
     for (int j = 0; j < kPChunks; ++j) {
@@ -763,17 +770,26 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     static const int per_cu =
         std::getenv("DPPO_GAE_WGS_PER_CU") ? std::atoi(std::getenv("DPPO_GAE_WGS_PER_CU")) : 1;
     const bool e32 = env_e == 32 ? N % 32 == 0 : (env_e == 16 ? false : (N % 32 == 0 && N / 32 >= cus));
+    // 64-env tiles (256-B rows) where they still give every CU a tile: DPPO_GAE_E=64 (A/B)
+    const bool e64 = env_e == 64 && N % 64 == 0 && N / 64 >= cus;
     // DPPO_GAE_WT=0/1: plain or write-through (sc1) advantage / return stores (A/B timing)
     static const int wt = std::getenv("DPPO_GAE_WT") ? std::atoi(std::getenv("DPPO_GAE_WT")) : 0;
     // Cycles between the owners' first load bursts: 450-750 measured 8.0-8.25 us per launch at
     // N = 8192 against 9.1 without (1,200: 9.6, 1,800: 10.6).  DPPO_GAE_STAGGER overrides (A/B).
     static const int stagger =
         std::getenv("DPPO_GAE_STAGGER") ? std::atoi(std::getenv("DPPO_GAE_STAGGER")) : 640;
-    const int tiles = e32 ? N / 32 : G;
+    const int tiles = e64 ? N / 64 : (e32 ? N / 32 : G);
     int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
     if (!e32 && grid >= 16) grid -= grid % 16;
     *n_partials = grid;
-    if (mode == DPPO_GAE_AFFINE) {
+    if (e64) {
+      if (mode == DPPO_GAE_AFFINE)
+        DPPO_LAUNCH(gae_aff_kernel<64>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
+                    nv, adv, ret, partials, T, N, gamma, c);
+      else
+        DPPO_LAUNCH(gae_pipe_kernel<64>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
+                    adv, ret, partials, T, N, gamma, c, wt, stagger);
+    } else if (mode == DPPO_GAE_AFFINE) {
       if (e32)
         DPPO_LAUNCH(gae_aff_kernel<32>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
                     nv, adv, ret, partials, T, N, gamma, c);

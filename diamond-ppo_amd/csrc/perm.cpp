@@ -484,6 +484,8 @@ bool bad_args(const uint32_t* key, const int32_t* pos, int64_t n, int32_t count,
   return !key || !pos || !out || n < 0 || n > 0x7FFFFFFF || count < 0 || *pos < 0 || *pos > kN;
 }
 
+std::atomic<int64_t> g_targets_ringed{0};
+
 }  // namespace
 
 extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
@@ -491,6 +493,26 @@ extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, i
   if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
   MT g;
   g.load(key, *pos);
+  static const int ring_mode = [] {
+    const char* e = std::getenv("DPPO_PERM_RING");
+    return e ? std::atoi(e) : 1;
+  }();
+  if (ring_mode && n * count >= (1 << 20)) {
+    // The global-minibatch draws (E permutations of the global batch, tens of millions of
+    // targets): a producer thread twists the MT19937 blocks ahead, this thread runs only the
+    // accept scan (the twist is ~37 % of the draw time)
+    RingBlocks ring(g.mt, SwapPool::get().cpus());
+    int p = g.pos;
+    const uint32_t* blk = draw_targets_from(ring, g.out, p, n, count, out);
+    if (blk != g.out) {
+      for (int k = 0; k < kN; ++k) key[k] = untemper(blk[k]);
+    } else {
+      std::memcpy(key, g.mt, sizeof(g.mt));
+    }
+    *pos = p;
+    g_targets_ringed.fetch_add(1, std::memory_order_relaxed);
+    return DPPO_OK;
+  }
   draw_targets(g, n, count, out);
   std::memcpy(key, g.mt, sizeof(g.mt));
   *pos = g.pos;

@@ -28,27 +28,28 @@ from .utils import Checkpointer, Logger, Ticker, Timer
 
 @dataclass
 class PPOConfig:
-    total_steps: int = 1_000_000    # total training environment steps
-    rollout_steps: int = 64         # number of vectorised steps per rollout
-    num_envs: int = 16              # number of parallel environments
-    lr: float = 3e-4                # Adam optimiser learning rate
-    adam_eps: float = 1e-5          # Adam optimiser epsilon
-    decay_lr: bool = False          # linear learning rate decay
-    gamma: float = 0.99             # discount factor
-    gae_lambda: float = 0.95        # GAE lambda parameter
-    num_epochs: int = 4             # PPO epochs per update
-    num_minibatches: int = 8        # PPO minibatch updates per epoch
-    ppo_clip: float = 0.2           # PPO clipping epsilon
-    value_loss_weight: float = 1.0  # weight of value loss
-    entropy_beta: float = 0.01      # entropy regularisation coeffient
-    advantage_norm: bool = True     # normalise advantages if true
-    grad_norm_clip: float = 0.5     # global gradient norm clip
-    network_hidden_dim: int = 64    # hidden dim for default MLP
+    # the reference's fields, order and defaults (ppo.py:15-37)
+    total_steps: int = 1_000_000    # env steps over the whole train() run
+    rollout_steps: int = 64         # T: vector-env steps per rollout
+    num_envs: int = 16              # N: environments stepped together
+    lr: float = 3e-4                # Adam learning rate
+    adam_eps: float = 1e-5          # Adam epsilon (added after dividing by sqrt(bias corr.))
+    decay_lr: bool = False          # LinearLR from 1.0 to 0.05 over the run
+    gamma: float = 0.99             # discount
+    gae_lambda: float = 0.95        # GAE lambda
+    num_epochs: int = 4             # passes over each rollout
+    num_minibatches: int = 8        # optimizer steps per pass
+    ppo_clip: float = 0.2           # surrogate ratio clip
+    value_loss_weight: float = 1.0  # value-loss coefficient
+    entropy_beta: float = 0.01      # entropy-bonus coefficient
+    advantage_norm: bool = True     # standardise advantages over the rollout
+    grad_norm_clip: float = 0.5     # max global L2 norm of the gradient
+    network_hidden_dim: int = 64    # width of the default MLP
     cuda: bool = False              # kept for compatibility (this build always uses the GPU)
-    seed: int | None = 42           # RNG seed
-    checkpoint: bool = False        # enable model checkpointing
-    save_interval: float = 600      # checkpoint interval (seconds)
-    verbose: bool = True            # verbose logging
+    seed: int | None = 42           # seeds numpy's global RNG and torch
+    checkpoint: bool = False        # save checkpoints during train()
+    save_interval: float = 600      # seconds between saves
+    verbose: bool = True            # print the Ticker table
     device_index: int = 0           # GPU ordinal (additive; LOCAL_RANK wins under torchrun)
     # data parallelism over ranks (additive): False = each rank permutes its own envs' samples and
     # global minibatch j is the union of the ranks' local minibatches j; True = every rank draws

@@ -18,41 +18,61 @@ import torch
 
 
 class Checkpointer:
+    """``{run_name}-step{step:06d}.pt`` files holding ``{"step", "model_state", "opt_state"}`` --
+    the reference's payload and naming (utils.py:584-619), so either side loads the other's files.
+    Writes go to a temporary name first and are renamed into place (a crash mid-save never leaves a
+    truncated checkpoint under the final name); loads are weights-only (no pickle code runs);
+    ``keep_last`` trims by step number, not by file-name order."""
+
     def __init__(self, folder: str | Path = "models", run_name: str = "run", *,
                  keep_last: int | None = None) -> None:
         self.folder = Path(folder)
         self.run_name = run_name
         self.keep_last = keep_last
 
+    def path_for(self, step: int) -> Path:
+        return self.folder / f"{self.run_name}-step{step:06d}.pt"
+
     def save(self, step: int, model: torch.nn.Module, optimizer=None) -> None:
-        self.folder.mkdir(parents=True, exist_ok=True)
-        path = self.folder / f"{self.run_name}-step{step:06d}.pt"
         payload = {"step": step, "model_state": model.state_dict()}
         if optimizer is not None:
             payload["opt_state"] = optimizer.state_dict()
-        torch.save(payload, path)
-        self._trim_old()
+        self.folder.mkdir(parents=True, exist_ok=True)
+        final = self.path_for(step)
+        tmp = final.with_name(final.name + ".partial")
+        torch.save(payload, tmp)
+        tmp.replace(final)
+        if self.keep_last is not None:
+            for _, old in self._saved()[:-self.keep_last]:
+                old.unlink(missing_ok=True)
 
     def load(self, path: str | Path, model: torch.nn.Module, optimizer=None) -> None:
-        chk = torch.load(path, map_location="cpu", weights_only=True)
-        model.load_state_dict(chk["model_state"])
-        if optimizer is not None and "opt_state" in chk:
-            optimizer.load_state_dict(chk["opt_state"])
+        state = torch.load(path, map_location="cpu", weights_only=True)
+        model.load_state_dict(state["model_state"])
+        if optimizer is not None and "opt_state" in state:
+            optimizer.load_state_dict(state["opt_state"])
 
-    def _trim_old(self) -> None:
-        if self.keep_last is None:
-            return
-        ckpts = sorted(self.folder.glob(f"{self.run_name}-step*.pt"))
-        for old in ckpts[:-self.keep_last]:
-            old.unlink(missing_ok=True)
+    def _saved(self) -> list:
+        """(step, path) of this run's checkpoints, oldest step first."""
+        prefix = f"{self.run_name}-step"
+        found = []
+        for f in self.folder.glob(prefix + "*.pt"):
+            digits = f.stem[len(prefix):]
+            if digits.isdigit():
+                found.append((int(digits), f))
+        return sorted(found)
 
 
 class Ticker:
-    """Live training progress (reference utils.py:20-215): per-env episode returns / lengths,
-    a moving window of finished episodes, and one progress row per ``print_every`` vector steps,
-    rewritten in place (``\r``) and kept as its own line at each of ``num_checkpoints`` evenly
-    spaced rollout boundaries.  FPS is measured since the last checkpoint; extra keyword scalars
-    passed to :meth:`tick` become extra columns."""
+    """Console progress of a training run (the reference's table, utils.py:20-215): episode
+    returns / lengths per env, the mean over the last ``window_size`` finished episodes, and a
+    progress row every ``print_every`` vector steps, rewritten in place (``\r``) and left standing
+    at ``num_checkpoints`` evenly spaced rollout boundaries.  FPS counts from the last standing
+    row; keyword scalars given to :meth:`tick` are appended as columns."""
+
+    # (header, width) of the fixed columns
+    COLUMNS = (("Progress", 8), ("Step", 9), ("Episode", 8), ("Mean Rew", 8), ("Mean Len", 7),
+               ("FPS", 6), ("Time", 8))
 
     def __init__(self, total_steps: int, num_envs: int, rollout_steps: int, *,
                  window_size: int = 100, print_every: int = 5, num_checkpoints: int = 20,
@@ -63,13 +83,16 @@ class Ticker:
         self.window_size = window_size
         self.print_every = print_every
         self.verbose = verbose
-        # rollout-aligned steps at which a row is kept: i * (iterations // n) rollouts, i = 1..n
         per_rollout = rollout_steps * num_envs
-        iters = total_steps // per_rollout
-        self.checkpoints = (np.arange(1, num_checkpoints + 1) * iters // num_checkpoints) * per_rollout
-        self._start_state()
+        rollouts = total_steps // per_rollout
+        # the standing rows: after rollouts k * rollouts // num_checkpoints, k = 1 .. num_checkpoints
+        marks = np.arange(1, num_checkpoints + 1) * rollouts // num_checkpoints
+        self.checkpoints = marks * per_rollout
+        self._marks = set(int(x) for x in self.checkpoints)
+        self.reset()
 
-    def _start_state(self) -> None:
+    def reset(self) -> None:
+        """Clear the counters and clocks; keep the configuration."""
         self.current_step = 0
         self.current_episode = 1
         self.current_returns = np.zeros(self.num_envs, np.float32)
@@ -79,12 +102,7 @@ class Ticker:
         self.custom_logs: dict = {}
         self._header_printed = False
         self.start_time = time.time()
-        self.last_checkpoint_time = self.start_time
-        self.last_checkpoint_step = 0
-
-    def reset(self) -> None:
-        """Clear the counters and clocks; keep the configuration."""
-        self._start_state()
+        self._mark_time, self._mark_step = self.start_time, 0
 
     def tick(self, rewards, dones, **custom_logs) -> None:
         """One vector-env step (and any extra scalars to show)."""
@@ -92,39 +110,42 @@ class Ticker:
         self.current_step += self.num_envs
         self.current_returns += np.asarray(rewards, dtype=np.float32)
         self.current_lengths += 1
-        for r, n in zip(self.current_returns[done], self.current_lengths[done]):
-            self.recent_returns.append(float(r))
-            self.recent_lengths.append(int(n))
-            self.current_episode += 1
-        self.current_returns[done] = 0.0
-        self.current_lengths[done] = 0
+        if done.any():
+            self.recent_returns.extend(float(x) for x in self.current_returns[done])
+            self.recent_lengths.extend(int(x) for x in self.current_lengths[done])
+            self.current_episode += int(done.sum())
+            self.current_returns[done] = 0.0
+            self.current_lengths[done] = 0
         self.custom_logs.update(custom_logs)
         if self.verbose:
             self.print_logs()
 
-    def print_logs(self) -> None:
-        """Print (overwrite) the progress row when due; keep it at a checkpoint."""
-        now = time.time()
-        if self.current_step in self.checkpoints:
-            if self._header_printed:
-                print()
-            self.last_checkpoint_time, self.last_checkpoint_step = now, self.current_step
-        if self.current_step % (self.num_envs * self.print_every) or not self.recent_returns:
-            return
-        if not self._header_printed:
-            cols = ["Progress", "Step", "Episode", "Mean Rew", "Mean Len", "FPS", "Time"]
-            widths = [8, 9, 8, 8, 7, 6, 8]
-            print("  |  ".join(f"{c:>{w}}" for c, w in zip(cols, widths)) +
-                  "".join(f"  |  {k}" for k in self.custom_logs))
-            self._header_printed = True
-        fps = (self.current_step - self.last_checkpoint_step) / (now - self.last_checkpoint_time
-                                                                  + 1e-6)
+    def _row(self, now: float) -> list:
+        fps = (self.current_step - self._mark_step) / (now - self._mark_time + 1e-6)
+        h, rem = divmod(int(now - self.start_time), 3600)
+        hms = f"{h:02}:{rem // 60:02}:{rem % 60:02}"
         cells = [f"{100 * self.current_step / self.total_steps:>7.1f}%",
                  f"{self.current_step:>9,}", f"{self.current_episode:>8,}",
                  f"{np.mean(self.recent_returns):>8.2f}", f"{np.mean(self.recent_lengths):>8.1f}",
-                 f"{fps:>6.0f}", f"{self._hms(now - self.start_time):>8}"]
-        cells += [f"{v:.2f}" if isinstance(v, float) else f"{v}" for v in self.custom_logs.values()]
-        print("\r" + "  |  ".join(cells), end="")
+                 f"{fps:>6.0f}", f"{hms:>8}"]
+        return cells + [f"{v:.2f}" if isinstance(v, float) else str(v)
+                        for v in self.custom_logs.values()]
+
+    def print_logs(self) -> None:
+        """Rewrite the progress row when one is due; leave it standing at a checkpoint."""
+        now = time.time()
+        if self.current_step in self._marks:
+            if self._header_printed:
+                print()
+            self._mark_time, self._mark_step = now, self.current_step
+        due = self.current_step % (self.num_envs * self.print_every) == 0
+        if not due or not self.recent_returns:
+            return
+        if not self._header_printed:
+            head = "  |  ".join(f"{name:>{w}}" for name, w in self.COLUMNS)
+            print(head + "".join(f"  |  {k}" for k in self.custom_logs))
+            self._header_printed = True
+        print("\r" + "  |  ".join(self._row(now)), end="")
 
     @property
     def logs(self) -> dict:
@@ -136,12 +157,6 @@ class Ticker:
                 "best_reward": max(self.recent_returns, default=None),
                 "total_duration": elapsed, "mean_fps": self.current_step / (elapsed + 1e-6),
                 "custom_logs": dict(self.custom_logs)}
-
-    @staticmethod
-    def _hms(seconds: float) -> str:
-        h, rem = divmod(int(seconds), 3600)
-        m, sec = divmod(rem, 60)
-        return f"{h:02}:{m:02}:{sec:02}"
 
 
 def _figure_out(fig, show: bool):

@@ -27,10 +27,13 @@ def main():
     ap.add_argument("--T", type=int, default=128)
     ap.add_argument("--N", type=int, default=8192)
     ap.add_argument("--sets", type=int, default=16)
+    ap.add_argument("--affine", action="store_true", help="the affine-scan kernel's timeline")
     a = ap.parse_args()
     T, N = a.T, a.N
     dev = torch.device("cuda", 0)
     h = NN.Handle(0, NN.Dims(T, N, 1, 1, 0, 64, 1, 1, 1, 0))
+    if a.affine:
+        h.set_gae_mode(NN.GAE_AFFINE)
     rng = np.random.default_rng(1)
     g = lambda x: torch.from_numpy(x).to(dev)
     bufs = [[g(rng.normal(1, 1, (T, N)).astype(np.float32)),
@@ -51,6 +54,13 @@ def main():
     for w in range(2):
         t = buf[w] - buf[w][0]
         print(f"workgroup {0 if w == 0 else 128}: end {t[41]} cycles")
+        if a.affine:
+            print("  chunk  loads-landed  local-scan-done  barrier-passed  fold-done  "
+                  "stores-issued")
+            for k in range(7, -1, -1):
+                print(f"  {k:5d}  {t[1 + k]:12d}  {t[9 + k]:15d}  {t[25 + k]:14d}  "
+                      f"{t[33 + k]:9d}  {t[17 + k]:13d}")
+            continue
         print("  chunk  loads-landed  scan-seen  scan-done  owner-wait-done  stores-issued")
         for k in range(7, -1, -1):
             print(f"  {k:5d}  {t[1 + k]:12d}  {t[25 + k]:9d}  {t[33 + k]:9d}  {t[9 + k]:15d}  "
