@@ -570,8 +570,17 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
     if (lane < E) {
       // the carry into this chunk: the later super-chunk's, then the later chunks' maps
       float cin = s == 0 ? 0.0f : L.carry[par][lane];
-      for (int j = kPChunks - 1; j > k; --j)
-        cin = gae_carry(L.B[par][j][lane], L.P[par][j][lane], cin);
+      // every map read first, then the <= 7 dependent steps (a rolled loop over j > k waited for
+      // each read: ~150 cycles per step)
+      float Bj[kPChunks], Pj[kPChunks];
+#pragma unroll
+      for (int j = 0; j < kPChunks; ++j) {
+        Bj[j] = L.B[par][j][lane];
+        Pj[j] = L.P[par][j][lane];
+      }
+#pragma unroll
+      for (int j = kPChunks - 1; j > 0; --j)
+        if (j > k) cin = gae_carry(Bj[j], Pj[j], cin);
       f32x4 av[4];
 #pragma unroll
       for (int j = 0; j < kPChunk; ++j) av[j >> 2][j & 3] = gae_carry(bl[j], pl[j], cin);
@@ -770,8 +779,9 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     static const int per_cu =
         std::getenv("DPPO_GAE_WGS_PER_CU") ? std::atoi(std::getenv("DPPO_GAE_WGS_PER_CU")) : 1;
     const bool e32 = env_e == 32 ? N % 32 == 0 : (env_e == 16 ? false : (N % 32 == 0 && N / 32 >= cus));
-    // 64-env tiles (256-B rows) where they still give every CU a tile: DPPO_GAE_E=64 (A/B)
-    const bool e64 = env_e == 64 && N % 64 == 0 && N / 64 >= cus;
+    // 64-env tiles (256-B rows) where they still give every CU a tile (N >= 16,384 on 256 CUs):
+    // at N = 65,536 41.0 us per launch against 43.6 with 32-env tiles (exact mode, same box)
+    const bool e64 = (env_e == 64 || env_e == 0) && N % 64 == 0 && N / 64 >= cus;
     // DPPO_GAE_WT=0/1: plain or write-through (sc1) advantage / return stores (A/B timing)
     static const int wt = std::getenv("DPPO_GAE_WT") ? std::atoi(std::getenv("DPPO_GAE_WT")) : 0;
     // Cycles between the owners' first load bursts: 450-750 measured 8.0-8.25 us per launch at

@@ -1000,6 +1000,12 @@ bool mbw_supported(const MlpShape& sh) {
   // 8-action instantiations spill registers and lose to the two-team kernel (HalfCheetah, D = 17,
   // A = 6: 92 vs 77 us per launch).
   if (legacy || sh.D > 32) return false;
+  // DPPO_MBW_CONT6=1 (A/B): 5-6 Gaussian actions on 17-32 inputs through the sample-split kernel
+  static const bool cont6 = [] {
+    const char* e = std::getenv("DPPO_MBW_CONT6");
+    return e && e[0] == '1';
+  }();
+  if (cont6 && sh.continuous && sh.A >= 5 && sh.A <= 6 && sh.D > 16) return true;
   return sh.A <= 4 || (sh.A <= 8 && !sh.continuous && sh.D <= 16);
 }
 
@@ -1053,7 +1059,7 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     DPPO_SETW(2, false, 1) DPPO_SETW(2, true, 1) DPPO_SETW(4, false, 1) DPPO_SETW(4, true, 1)
     DPPO_SETW(2, false, 2) DPPO_SETW(2, true, 2) DPPO_SETW(4, false, 2) DPPO_SETW(4, true, 2)
-    DPPO_SETW(8, false, 1)
+    DPPO_SETW(8, false, 1) DPPO_SETW(6, true, 2)
 #undef DPPO_SETW
   }
   const dim3 grid((unsigned)G), block(kThreadsW);
@@ -1072,6 +1078,7 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
   } while (0)
   if (sh.A <= 2) DPPO_LWC(2);
   else if (sh.A <= 4) DPPO_LWC(4);
+  else if (c) DPPO_LW(6, true, 2);  // mbw_supported: 5-6 Gaussian actions, 17-32 inputs
   else DPPO_LW(8, false, 1);  // mbw_supported: discrete, D <= 16
 #undef DPPO_LWC
 #undef DPPO_LW

@@ -493,14 +493,15 @@ extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, i
   if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
   MT g;
   g.load(key, *pos);
+  // DPPO_PERM_TARGETS_RING=1 (A/B only): a producer thread twists the MT19937 blocks ahead of
+  // this accept scan.  Off by default: on the GPU box's EPYC 9575F the 4 x 8.4 M-target draw of
+  // C5's global minibatches took 65 ms with the ring against 15.8 ms on one thread (the AVX-512
+  // twist is cheap next to the scan, and the hand-off lines cost more than they save).
   static const int ring_mode = [] {
-    const char* e = std::getenv("DPPO_PERM_RING");
-    return e ? std::atoi(e) : 1;
+    const char* e = std::getenv("DPPO_PERM_TARGETS_RING");
+    return e ? std::atoi(e) : 0;
   }();
   if (ring_mode && n * count >= (1 << 20)) {
-    // The global-minibatch draws (E permutations of the global batch, tens of millions of
-    // targets): a producer thread twists the MT19937 blocks ahead, this thread runs only the
-    // accept scan (the twist is ~37 % of the draw time)
     RingBlocks ring(g.mt, SwapPool::get().cpus());
     int p = g.pos;
     const uint32_t* blk = draw_targets_from(ring, g.out, p, n, count, out);

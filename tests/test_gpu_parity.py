@@ -74,7 +74,8 @@ def test_gae_bitexact_golden():
 
 
 @pytest.mark.parametrize("T,Nn", [(128, 8192), (128, 4096), (300, 16), (1, 1), (129, 33),
-                                  (7, 4104), (200, 8448), (64, 6144), (16, 12288)])
+                                  (7, 4104), (200, 8448), (64, 6144), (16, 12288),
+                                  (128, 65536), (200, 16384), (64, 16448)])
 def test_gae_vs_oracle_sizes(T, Nn):
     from oracle import ppo_np as P
     rng = np.random.default_rng(T * 31 + Nn)
