@@ -116,6 +116,8 @@ struct WArgs {
   float* slabs;
   int64_t slab_stride, p_total;
   int D, D8, A, R, nkn;
+  int plain_slab;  // DPPO_SLAB_PLAIN=1 (A/B): plain slab stores (L2-resident, written back at the
+                   // kernel boundary) instead of write-through
 };
 
 constexpr WLds make_wlds(int D16) {
@@ -858,7 +860,9 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       const f32x4 v = ((((const f32x4*)stg)[c] + ((const f32x4*)(stg + kMat))[c]) +
                        ((const f32x4*)(stg + 2 * kMat))[c]) +
                       ((const f32x4*)(stg + 3 * kMat))[c];
-      slab_st4(slab + off + 4 * c, scale == 1.0f ? v : v * scale);
+      const f32x4 w = scale == 1.0f ? v : v * scale;
+      if (a.plain_slab) *(f32x4*)(slab + off + 4 * c) = w;
+      else slab_st4(slab + off + 4 * c, w);
     }
   };
   // a whole hidden matrix: all sixteen LDS reads of a thread in flight before the first add
@@ -872,7 +876,9 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
     for (int i = 0; i < kIt; ++i) {
       const f32x4 v = ((x[i][0] + x[i][1]) + x[i][2]) + x[i][3];
-      slab_st4(slab + off + 4 * (tid + i * kThreadsW), scale == 1.0f ? v : v * scale);
+      const f32x4 w = scale == 1.0f ? v : v * scale;
+      if (a.plain_slab) *(f32x4*)(slab + off + 4 * (tid + i * kThreadsW)) = w;
+      else slab_st4(slab + off + 4 * (tid + i * kThreadsW), w);
     }
   };
   // register-only reductions of this wave's small items first (they overlap the wait for the
@@ -1046,6 +1052,11 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
   k.A = sh.A;
   k.R = sh.R;
   k.nkn = (sh.D + 3) / 4;
+  static const int plain = [] {
+    const char* e = std::getenv("DPPO_SLAB_PLAIN");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  k.plain_slab = plain;
   const size_t lds = mbw_lds_bytes(sh);
   if (lds > 160 * 1024) {
     set_error("minibatch kernel needs %zu bytes of LDS (> 160 KiB)", lds);

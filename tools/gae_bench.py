@@ -26,10 +26,13 @@ def main():
     ap.add_argument("--N", type=int, default=8192)
     ap.add_argument("--sets", type=int, default=16)
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--affine", action="store_true", help="the affine-scan (tolerance) mode")
     a = ap.parse_args()
     T, N = a.T, a.N
     dev = torch.device("cuda", 0)
     h = NN.Handle(0, NN.Dims(T, N, 1, 1, 0, 64, 1, 1, 1, 0))
+    if a.affine:
+        h.set_gae_mode(NN.GAE_AFFINE)
     rng = np.random.default_rng(1)
     bufs = []
     for _ in range(a.sets):

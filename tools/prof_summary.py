@@ -55,10 +55,15 @@ def main():
     ap.add_argument("prof_dir")
     ap.add_argument("tag")
     ap.add_argument("--config", default="cartpole4096")
+    ap.add_argument("--gae", type=int, default=0,
+                    help="summarise a GAE-only run (gkt, gpmc3, gpmc4 under prof_dir) at this N")
+    ap.add_argument("--affine", action="store_true", help="(with --gae) the affine-scan mode")
     a = ap.parse_args()
     P = a.prof_dir
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
+    if a.gae:
+        return gae_summary(P, a.tag, a.gae, a.affine, out_dir)
     stats_src = os.path.join(P, "kt", "kt_kernel_stats.csv")
     shutil.copy(stats_src, os.path.join(out_dir, f"{a.tag}_kernel_stats.csv"))
     lines = [f"# {a.tag}: rocprofv3 summary ({a.config})", ""]
@@ -181,6 +186,45 @@ def main():
                 if ln.startswith("{"):
                     lines += ["", "```", ln.strip(), "```"]
     open(os.path.join(out_dir, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+def gae_summary(P, tag, N, affine, out_dir):
+    """One GAE-only run (tools/gae_bench.py under rocprofv3): kernel stats and HBM traffic per
+    launch, keyed gae<N>[_affine] in pmc_traffic.json."""
+    key = f"gae{N}" + ("_affine" if affine else "")
+    gstats = os.path.join(P, "gkt", "gkt_kernel_stats.csv")
+    shutil.copy(gstats, os.path.join(out_dir, f"{tag}_{key}_kernel_stats.csv"))
+    lines = [f"# {tag}: GAE at num_envs = {N}" + (" (affine-scan mode)" if affine else ""), "",
+             "| kernel | calls | avg µs | min µs | max µs |", "|---|---|---|---|---|"]
+    for r in csv.DictReader(open(gstats)):
+        if base(r["Name"]).startswith("gae_"):
+            lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | "
+                         f"{float(r['AverageNs']) / 1e3:.2f} | {float(r['MinNs']) / 1e3:.2f} | "
+                         f"{float(r['MaxNs']) / 1e3:.2f} |")
+    g = {}
+    for k in ("gpmc3/g3", "gpmc4/g4"):
+        f = os.path.join(P, k + "_counter_collection.csv")
+        if os.path.exists(f):
+            for kern, d in load_pmc(f).items():
+                if base(kern).startswith("gae_"):
+                    g.update(d)
+    if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
+        rd, wr = 2 * g["FETCH_SIZE"] * 1024, g["WRITE_SIZE"] * 1024
+        alg_r, alg_w = 14 * 128 * N, 8 * 128 * N
+        lines += ["", f"HBM traffic per launch: read {rd / 1e6:.2f} MB (2 x FETCH_SIZE), write "
+                  f"{wr / 1e6:.2f} MB (algorithmic: 14 B + 8 B per element = {alg_r / 1e6:.2f} + "
+                  f"{alg_w / 1e6:.2f} MB; ratio {(rd + wr) / (alg_r + alg_w):.3f})"]
+        pj = os.path.join(out_dir, "pmc_traffic.json")
+        allt = json.load(open(pj)) if os.path.exists(pj) else {}
+        allt[key] = {"gae": int(rd + wr)}
+        json.dump(allt, open(pj, "w"), indent=1, sort_keys=True)
+    glog = os.path.join(P, "gkt.log")
+    if os.path.exists(glog):
+        for ln in open(glog):
+            if ln.startswith("{"):
+                lines += ["", "```", ln.strip(), "```"]
+    open(os.path.join(out_dir, f"{tag}_{key}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
