@@ -401,10 +401,16 @@ struct GRec {
   f32x4 xt[NIB];      // T layout of the input: feature 16ib + r of samples 4q + v
   f32x4 sc;           // {action bits, old log-prob, advantage, return} of sample r
   f32x4 ca[2];        // continuous action of sample r (<= 8 dims)
+  int sn;             // sample r's record (kLateCa: the action is read in the group's phase 3)
 };
 
-template <int AMAX, bool CONT, int NIB>
+// X1: exactly 17 inputs (HalfCheetah).  Input column 16 is the only live one of the second
+// 16-column block, so its dW1 column is a VALU rank-1 sum (16 FMAs per group) instead of four
+// 16x16 MFMA tiles (16 MFMAs and 16 accumulator registers per group) -- the registers that
+// made this instantiation spill.
+template <int AMAX, bool CONT, int NIB, bool X1 = false>
 __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
+  static_assert(!X1 || NIB == 2, "X1 is the 17-input layout");
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #ifdef DPPO_PHASE_TRACE
   WEDGE(0, (long long)__builtin_amdgcn_s_memtime());
@@ -427,6 +433,15 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   const int stride = (int)gridDim.x * kWavesW;
   const int nk = first < ngroups ? (ngroups - first + stride - 1) / stride : 0;
   const int R = a.R, D = a.D;
+  // 5-8 Gaussian actions: the action is loaded at the start of its group's head layers instead
+  // of a group ahead (8 registers fewer across the backward phases, where this kernel spills)
+  constexpr bool kLateCa = CONT && (AMAX > 4 || NIB == 2);
+  // ... and the T-layout input for dW1 (indices and records) is read in the group's own phase 7,
+  // ~12 K cycles before its use, instead of being carried from the previous group
+  constexpr bool kLateXt = kLateCa;
+  // ... and the head-weight gradient is an MFMA tile sum (head rows x 64 features, 16 accumulator
+  // registers) instead of AMAX x 4 VALU partials per lane
+  constexpr bool kMfmaWo = kLateCa;
 
   // Loads never branch and loaded values are never selected on (which would wait for them):
   // out-of-range positions read a valid address instead -- a sample past m reads sample m - 1
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int st = g0 + 4 * q + v;
-      f.st[v] = idxp[st < mm ? st : mm - 1];
+      f.st[v] = kLateXt ? 0 : idxp[st < mm ? st : mm - 1];
     }
     return f;
   };
@@ -457,11 +472,12 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int c = 16 * ib + r;
-        g.xt[ib][v] = a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
+        g.xt[ib][v] = kLateXt ? 0.f : a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
       }
     g.sc = *(const f32x4*)(rn + a.D8);
-    g.ca[0] = CONT ? *(const f32x4*)(rn + a.D8 + 4) : z4();
-    g.ca[1] = (CONT && AMAX > 4) ? *(const f32x4*)(rn + a.D8 + 8) : z4();
+    g.ca[0] = CONT && !kLateCa ? *(const f32x4*)(rn + a.D8 + 4) : z4();
+    g.ca[1] = (CONT && !kLateCa && AMAX > 4) ? *(const f32x4*)(rn + a.D8 + 8) : z4();
+    g.sn = f.sn;
     return g;
   };
 
@@ -553,16 +569,20 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   float* sy = sx + kSlot;                           // c1 (N -> P), then dzc
   float* sd = sy + kSlot;                           // {dlogit[0..3], dvalue} per sample
 
-  f32x4 gW2[16], gWa[16], gWc[16], gW1[4 * NIB];
+  constexpr int NB1 = X1 ? 1 : NIB;  // input blocks of dW1 on MFMA tiles
+  f32x4 gW2[16], gWa[16], gWc[16], gW1[4 * NB1];
 #pragma unroll
   for (int i = 0; i < 16; ++i) gW2[i] = gWa[i] = gWc[i] = z4();
 #pragma unroll
-  for (int i = 0; i < 4 * NIB; ++i) gW1[i] = z4();
+  for (int i = 0; i < 4 * NB1; ++i) gW1[i] = z4();
+  f32x4 gx1 = z4();  // X1: dW1[4r + b][16] partial over this lane's samples 4q + v
   // P-form partials (component b = feature 4r + b, summed over this lane's samples 4q + v)
   f32x4 gb1 = z4(), gb2 = z4(), gba = z4(), gbc = z4(), gWv = z4();
-  f32x4 gWo[AMAX];
+  f32x4 gWo[kMfmaWo ? 1 : AMAX];
 #pragma unroll
-  for (int h = 0; h < AMAX; ++h) gWo[h] = z4();
+  for (int h = 0; h < (kMfmaWo ? 1 : AMAX); ++h) gWo[h] = z4();
+  // kMfmaWo: tile cb, lane (q, r), register i = dWo[head 4q + i][feature 4r + cb]
+  f32x4 gWoT[4] = {z4(), z4(), z4(), z4()};
   float gbo[AMAX], gls[AMAX], gbv = 0.f, s_pi = 0.f, s_v = 0.f, s_ent = 0.f;
 #pragma unroll
   for (int h = 0; h < AMAX; ++h) gbo[h] = gls[h] = 0.f;
@@ -621,6 +641,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) c1[ob] = *(const f32x4*)(lds + L.bc + 16 * ob + 4 * q);
     float out[AMAX];
+    if (kLateCa) {
+      const float* rn = a.rec + (int64_t)g_cur.sn * R + a.D8;
+      g_cur.ca[0] = *(const f32x4*)(rn + 4);
+      g_cur.ca[1] = *(const f32x4*)(rn + 8);
+    }
     SG_FENCE();
     {
       fwd64_raw(c1, Wc, h2, q, r);
@@ -742,6 +767,17 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       get_p(c1t, sy, q, r);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
+        if (kMfmaWo) {
+          // A operand: the delta of head r of sample 4q + v (rows past the heads are zero)
+          const float dr = sd[kSdw * (4 * q + v) + (r < AMAX ? r : 0)] * (r < AMAX ? 1.f : 0.f);
+          const float dvs = sd[kSdw * (4 * q + v) + kDv];
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            gWoT[cb] = mfma4(dr, a1t[cb][v], gWoT[cb]);
+            gWv[cb] += dvs * c1t[cb][v];
+          }
+          continue;
+        }
         f32x4 d4[NDL / 4];
 #pragma unroll
         for (int c = 0; c < NDL / 4; ++c) d4[c] = *(const f32x4*)(sd + kSdw * (4 * q + v) + 4 * c);
@@ -769,6 +805,21 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     PHASE_FENCE();
     WSTAMP(k, 5);
     // ---- (7) dh2 = Wa^T dza + Wc^T dzc (P layout)
+    if (kLateXt) {
+      int st[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int j = g0 + 4 * q + v;
+        st[v] = idxp[j < mm ? j : mm - 1];
+      }
+#pragma unroll
+      for (int ib = 0; ib < NIB; ++ib)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int c = 16 * ib + r;
+          g_cur.xt[ib][v] = a.rec[(int64_t)st[v] * R + (c < D ? c : D - 1)];
+        }
+    }
     f32x4 dh2[4] = {z4(), z4(), z4(), z4()};
     bwdP(dh2, Wa, dza, q, r);
     bwdP(dh2, Wc, dzc, q, r);
@@ -815,7 +866,14 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         dz1t[b] = dh1[b] * (1.0f - h1t[b] * h1t[b]);
         gb1[b] += (dz1t[b][0] + dz1t[b][1]) + (dz1t[b][2] + dz1t[b][3]);
       }
-      wgrad<NIB>(gW1, dz1t, g_cur.xt);
+      wgrad<NB1>(gW1, dz1t, g_cur.xt);
+      if (X1) {
+        // g_cur.xt[1][v] = input 16 of sample 4q + v in every lane (columns past 16 clamp to it)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) gx1[b] += dz1t[b][v] * g_cur.xt[1][v];
+      }
     }
     g_cur = g_nxt;
     PHASE_FENCE();
@@ -842,18 +900,23 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         *(f32x4*)(s + (16 * q + 4 * v + ob) * H + 4 * r) =
             (f32x4){acc[ob * 4 + 0][v], acc[ob * 4 + 1][v], acc[ob * 4 + 2][v], acc[ob * 4 + 3][v]};
   };
+  float x1s[4];  // X1: the summed column-16 partials (filled below)
   auto put_w1 = [&](float* stg, const f32x4* acc) {
     float* s = stg + wave * kMat;
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-      for (int ib = 0; ib < NIB; ++ib) {
+      for (int ib = 0; ib < NB1; ++ib) {
         const int col = 16 * ib + r;
         if (col < D) {
 #pragma unroll
-          for (int v = 0; v < 4; ++v) s[(16 * q + 4 * v + ob) * D + col] = acc[ob * NIB + ib][v];
+          for (int v = 0; v < 4; ++v) s[(16 * q + 4 * v + ob) * D + col] = acc[ob * NB1 + ib][v];
         }
       }
+    if (X1 && q == 0) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) s[(4 * r + b) * D + 16] = x1s[b];
+    }
   };
   auto sum_mat = [&](const float* stg, int64_t off, int n4, float scale) {
     for (int c = tid; c < n4; c += kThreadsW) {
@@ -887,13 +950,14 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   float xs[4][5 + AMAX];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
+    x1s[b] = X1 ? qsum(gx1[b]) : 0.f;
     xs[b][0] = qsum(gb1[b]);
     xs[b][1] = qsum(gb2[b]);
     xs[b][2] = qsum(gba[b]);
     xs[b][3] = qsum(gbc[b]);
     xs[b][4] = qsum(gWv[b]);
 #pragma unroll
-    for (int h = 0; h < AMAX; ++h) xs[b][5 + h] = qsum(gWo[h][b]);
+    for (int h = 0; h < AMAX; ++h) xs[b][5 + h] = kMfmaWo ? 0.f : qsum(gWo[h][b]);
   }
   float sc[2 * AMAX + 4];
 #pragma unroll
@@ -921,10 +985,19 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         s[1 * H + f] = xs[b][1];
         s[2 * H + f] = xs[b][2];
         s[3 * H + f] = xs[b][3];
+        if (!kMfmaWo) {
 #pragma unroll
-        for (int h = 0; h < AMAX; ++h) s[4 * H + h * H + f] = xs[b][5 + h];
+          for (int h = 0; h < AMAX; ++h) s[4 * H + h * H + f] = xs[b][5 + h];
+        }
         s[(4 + AMAX) * H + f] = xs[b][4];
       }
+    }
+    if (kMfmaWo && 4 * q < AMAX) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * q + i < AMAX) s[4 * H + (4 * q + i) * H + 4 * r + cb] = gWoT[cb][i];
     }
     if (lane == 0) {
 #pragma unroll
@@ -1002,16 +1075,21 @@ bool mbw_supported(const MlpShape& sh) {
     const char* e = std::getenv("DPPO_MB_LEGACY");
     return e && e[0] == '1' ? 1 : 0;
   }();
-  // Up to 4 actions at any input width; 5-8 only for discrete heads on <= 16 inputs: the other
-  // 8-action instantiations spill registers and lose to the two-team kernel (HalfCheetah, D = 17,
-  // A = 6: 92 vs 77 us per launch).
+  // Up to 4 actions at any input width; 5-8 for discrete heads on <= 16 inputs; 5-6 Gaussian
+  // actions on exactly 17 inputs (HalfCheetah: the X1 instantiation, spill-free, 74 vs 77.5 us per
+  // launch of the two-team kernel).  The rest goes to the two-team kernel: their sample-split
+  // instantiations spill.
   if (legacy || sh.D > 32) return false;
-  // DPPO_MBW_CONT6=1 (A/B): 5-6 Gaussian actions on 17-32 inputs through the sample-split kernel
-  static const bool cont6 = [] {
+  // DPPO_MBW_CONT6 (A/B): 0 sends the 17-input shape to the two-team kernel too, 1 sends 5-6
+  // Gaussian actions on any 17-32 inputs to the sample-split kernel
+  static const int cont6 = [] {
     const char* e = std::getenv("DPPO_MBW_CONT6");
-    return e && e[0] == '1';
+    return e && e[0] ? e[0] - '0' : -1;
   }();
-  if (cont6 && sh.continuous && sh.A >= 5 && sh.A <= 6 && sh.D > 16) return true;
+  if (sh.continuous && sh.A >= 5 && sh.A <= 6 && sh.D > 16) {
+    if (cont6 == 1) return true;
+    return cont6 != 0 && sh.D == 17;
+  }
   return sh.A <= 4 || (sh.A <= 8 && !sh.continuous && sh.D <= 16);
 }
 
@@ -1071,6 +1149,8 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
     DPPO_SETW(2, false, 1) DPPO_SETW(2, true, 1) DPPO_SETW(4, false, 1) DPPO_SETW(4, true, 1)
     DPPO_SETW(2, false, 2) DPPO_SETW(2, true, 2) DPPO_SETW(4, false, 2) DPPO_SETW(4, true, 2)
     DPPO_SETW(8, false, 1) DPPO_SETW(6, true, 2)
+    (void)hipFuncSetAttribute((const void*)mbw_kernel<6, true, 2, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 #undef DPPO_SETW
   }
   const dim3 grid((unsigned)G), block(kThreadsW);
@@ -1089,6 +1169,7 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
   } while (0)
   if (sh.A <= 2) DPPO_LWC(2);
   else if (sh.A <= 4) DPPO_LWC(4);
+  else if (c && sh.D == 17) DPPO_LAUNCH((mbw_kernel<6, true, 2, true>), grid, block, lds, s, k);
   else if (c) DPPO_LW(6, true, 2);  // mbw_supported: 5-6 Gaussian actions, 17-32 inputs
   else DPPO_LW(8, false, 1);  // mbw_supported: discrete, D <= 16
 #undef DPPO_LWC

@@ -81,6 +81,8 @@ def nit_of(m):
 
 def sample_split(D, A, cont):
     """Whether learn() runs the sample-split kernel (mbwave.hip, mbw_supported) for this shape."""
+    if cont and 5 <= A <= 6 and D == 17:
+        return True  # the X1 instantiation (HalfCheetah)
     return D <= 32 and (A <= 4 or (A <= 8 and not cont and D <= 16))
 
 

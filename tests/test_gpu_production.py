@@ -1,23 +1,25 @@
 """GPU parity of the minibatch kernels in their PRODUCTION configuration.
 
 Two kernels compute a minibatch gradient (csrc/common.h launch_mb):
-* the sample-split kernel (csrc/mbwave.hip; <= 4 actions, or <= 8 discrete on <= 16 inputs):
+* the sample-split kernel (csrc/mbwave.hip; <= 4 actions, <= 8 discrete on <= 16 inputs, or
+  HalfCheetah's 5-6 Gaussian actions on exactly 17 inputs -- the X1 instantiation):
   G = min(ceil(m/64), 256) workgroups of 4 waves, each wave running ceil(ceil(m/16) / 4G)
   16-sample groups end to end and accumulating its own weight gradients across them (C2: 4
   groups per wave, C3: 8).  The golden-trace tests have minibatches of at most 4,096 samples, i.e.
   one group per wave: the cross-group accumulation and prefetch are first exercised here;
-* the two-team kernel (csrc/mbstep.hip; HalfCheetah's 6 continuous actions on 17 inputs):
+* the two-team kernel (csrc/mbstep.hip; the other 5-8-action shapes, e.g. 6 Gaussian actions on
+  20 inputs; HalfCheetah too under DPPO_MBW_CONT6=0):
   G = min(ceil(m/32), 256) workgroups, each running nit = ceil(ceil(m/32)/G) 32-sample steps
   through a two-team software pipeline (the forward team on step it while the backward team
   back-propagates step it-1, hand-off images double-buffered by step parity); small minibatches
-  have nit == 1 and never read the odd-parity buffers.  C4 runs nit = 8.
+  have nit == 1 and never read the odd-parity buffers.
 These tests run the production shapes:
 
 * one minibatch gradient at the full C2 / C3 / C4 minibatch sizes (65,536 / 131,072 / 65,536
-  samples, nit = 8 / 16 / 8), plus a ragged one (m % 32 != 0, workgroups with unequal step
+  samples: 4 / 8 / 4 groups per wave), plus a ragged one (m % 32 != 0, workgroups with unequal step
   counts), through ``dppo_minibatch_grad_f32`` against the oracle's ``minibatch_loss_grads`` on the
   same sample records and indices (reference ppo.py:261-283, continuous_ppo.py:273-295);
-* a full ``learn()`` at intermediate sizes (nit = 2 and 3, discrete and continuous) and at the full
+* a full ``learn()`` at intermediate sizes (depth 1-3, both kernels, discrete and continuous) and at the full
   C2 size (nit = 8) against the oracle's ``learn`` with the same NumPy permutations
   (ppo.py:224-287).
 
@@ -182,7 +184,8 @@ def learn_vs_oracle(T, Nn, D, A, cont, seed):
     (100, 3000, 5, 3, False, 3),     # mb 37,500: three groups per wave, the last group partial
     (100, 1000, 5, 3, False, 1),     # mb 12,500: 196 workgroups, the last group partial
     (128, 2048, 3, 1, True, 2),      # Gaussian head on the sample-split kernel
-    (128, 768, 17, 6, True, 2),      # two-team kernel: 384 steps over 256 workgroups (ragged nit)
+    (128, 1536, 17, 6, True, 2),     # HalfCheetah's X1 sample-split kernel: some waves two groups
+    (128, 768, 20, 6, True, 2),      # two-team kernel: 384 steps over 256 workgroups (ragged nit)
 ])
 def test_learn_intermediate_depth_vs_oracle(T, Nn, D, A, cont, want_depth):
     mb = learn_vs_oracle(T, Nn, D, A, cont, seed=T + Nn)
