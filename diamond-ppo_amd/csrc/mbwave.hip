@@ -240,19 +240,31 @@ __device__ __forceinline__ float dot4(f32x4 w, f32x4 x) {
   return (w[0] * x[0] + w[1] * x[1]) + (w[2] * x[2] + w[3] * x[3]);
 }
 
+// DPPO_ABL_NOCONFLICT (timing-only ablation, wrong results): the hidden-weight and scratch
+// ds_read_b128 of the main loop read addresses that keep every lane group on distinct banks
+// (lanes with the same r read the same 16 B), to bound what the 2-way conflicts of the real
+// layout cost.
+#ifdef DPPO_ABL_NOCONFLICT
+#define ABL_FWD(q, r) (4 * (r))
+#define ABL_BWD(q, r) (4 * (r))
+#else
+#define ABL_FWD(q, r) ((r) * kWS + 4 * (q))
+#define ABL_BWD(q, r) (4 * (q) * kWS + 4 * (r))
+#endif
+
 // Forward of one hidden layer, N -> N: y[ob] += W[16ob + i][:] x for the four 16-row output
 // blocks; the A operand of k-steps (kb, 0..3) is one ds_read_b128 of the row.
 __device__ __forceinline__ void fwd64_raw(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4],
                                           int q, int r) {
   f32x4 w[2][4];
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) w[0][ob] = *(const f32x4*)(W + (16 * ob + r) * kWS + 4 * q);
+  for (int ob = 0; ob < 4; ++ob) w[0][ob] = *(const f32x4*)(W + 16 * ob * kWS + ABL_FWD(q, r));
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
     if (kb + 1 < 4) {
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob)
-        w[(kb + 1) & 1][ob] = *(const f32x4*)(W + (16 * ob + r) * kWS + 16 * (kb + 1) + 4 * q);
+        w[(kb + 1) & 1][ob] = *(const f32x4*)(W + 16 * ob * kWS + 16 * (kb + 1) + ABL_FWD(q, r));
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v)
@@ -283,7 +295,7 @@ __device__ __forceinline__ void fwd64x2(f32x4 (&y)[4], const float* W, f32x4 (&z
   f32x4 w[2][4], u[2][4];
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
-    const int o = (16 * ob + r) * kWS + 4 * q;
+    const int o = 16 * ob * kWS + ABL_FWD(q, r);
     w[0][ob] = *(const f32x4*)(W + o);
     u[0][ob] = *(const f32x4*)(U + o);
   }
@@ -292,7 +304,7 @@ __device__ __forceinline__ void fwd64x2(f32x4 (&y)[4], const float* W, f32x4 (&z
     if (kb + 1 < 4) {
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) {
-        const int o = (16 * ob + r) * kWS + 16 * (kb + 1) + 4 * q;
+        const int o = 16 * ob * kWS + 16 * (kb + 1) + ABL_FWD(q, r);
         w[(kb + 1) & 1][ob] = *(const f32x4*)(W + o);
         u[(kb + 1) & 1][ob] = *(const f32x4*)(U + o);
       }
@@ -323,7 +335,7 @@ __device__ __forceinline__ void bwdP(f32x4 (&t)[4], const float* W, const f32x4 
   SG_FENCE();
   f32x4 b[3];
   auto ld = [&](int k) {
-    return *(const f32x4*)(W + (16 * (k >> 2) + 4 * q + (k & 3)) * kWS + 4 * r);
+    return *(const f32x4*)(W + (16 * (k >> 2) + (k & 3)) * kWS + ABL_BWD(q, r));
   };
   b[0] = ld(0);
   b[1] = ld(1);
@@ -365,7 +377,11 @@ __device__ __forceinline__ void put_n(float* sm, const f32x4 (&n)[4], int q, int
 __device__ __forceinline__ void get_p(f32x4 (&t)[4], const float* sm, int q, int r) {
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
+#ifdef DPPO_ABL_NOCONFLICT
+    const f32x4 x = *(const f32x4*)(sm + v * kSm + 4 * r);
+#else
     const f32x4 x = *(const f32x4*)(sm + (4 * q + v) * kSm + 4 * r);
+#endif
 #pragma unroll
     for (int b = 0; b < 4; ++b) t[b][v] = x[b];
   }
@@ -378,7 +394,11 @@ __device__ __forceinline__ void put_p(float* sm, const f32x4 (&t)[4], int q, int
 }
 __device__ __forceinline__ void get_n(f32x4 (&n)[4], const float* sm, int q, int r) {
 #pragma unroll
+#ifdef DPPO_ABL_NOCONFLICT
+  for (int ob = 0; ob < 4; ++ob) n[ob] = *(const f32x4*)(sm + 16 * ob + 4 * r);
+#else
   for (int ob = 0; ob < 4; ++ob) n[ob] = *(const f32x4*)(sm + r * kSm + 16 * ob + 4 * q);
+#endif
 }
 
 __device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
@@ -608,7 +628,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     put_n(sh1, h, q, r);
   };
   // (only where the registers allow it: the other instantiations would spill)
-  constexpr bool kHoistL1 = AMAX == 2 && !CONT && NIB == 1;
+  constexpr bool kHoistL1 = !CONT && NIB == 1 && AMAX <= 4;
   f32x4 h1[4];
   if (kHoistL1 && nk > 0) layer1(h1, g_cur);
   PHASE_FENCE();
