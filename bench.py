@@ -337,6 +337,10 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
                    "obs_dim": D, "act_dim": A, "continuous": cont, "hidden": H,
                    "batch_per_learn": B_global, "minibatch": B_global // M,
                    "parallelism": f"env-axis dp{world}",
+                   # the per-minibatch gradient exchange: the one-shot peer all-reduce over the
+                   # ranks' xGMI-mapped buffers, or RCCL (DPPO_COMM, engine._init_comm)
+                   "exchange": ("peer" if getattr(agent._learner, "peer", False) else "rccl")
+                               if world > 1 else "none",
                    "minibatches": "global" if (global_mb and world > 1) else
                                   ("local-union" if world > 1 else "reference")},
         "roofline": roofline,

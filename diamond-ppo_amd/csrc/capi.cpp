@@ -154,6 +154,15 @@ struct dppo_handle {
   void* loop_out = nullptr;
   size_t loop_bytes = 0;
   hipEvent_t loop_ready = nullptr, loop_done = nullptr;
+  // peer exchange (peer.hip): this rank's exchange buffer, and every rank's as mapped here
+  char* xbuf = nullptr;
+  int64_t xcap = 0;                  // elements (of up to 8 B) per parity
+  char* xpeer[kMaxPeers] = {};
+  bool xmapped[kMaxPeers] = {};      // opened with hipIpcOpenMemHandle (closed on teardown)
+  int xworld = 0;                    // > 0: the exchange carries every all-reduce
+  bool xfused = false;               // the gradient exchange runs inside reduce_adam_kernel
+  unsigned xseq = 0;                 // exchanges so far (the same count on every rank)
+  unsigned long long xticks = 0;     // wait bound of one exchange (s_memrealtime ticks)
 };
 
 namespace {
@@ -254,6 +263,12 @@ inline hipStream_t S(void* s) { return (hipStream_t)s; }
 int device_status(const dppo_handle* h) {
   const unsigned e = h->err_host ? __atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) : 0u;
   if (e == 0u) return DPPO_OK;
+  if (e == kErrPeerTimeout) {
+    set_error("a peer exchange timed out: another rank did not reach the same all-reduce within "
+              "%.0f s (DPPO_PEER_TIMEOUT_S); that optimizer step used this rank's gradient alone "
+              "and this handle is no longer usable", (double)h->xticks / 1e8);
+    return DPPO_ECOMM;
+  }
   set_error("a grid-wide fan-in timed out (code %u): its workgroups were not all resident on the "
             "device at once (another process holding the CUs, or a partitioned device); the "
             "parameters of that optimizer step were left unchanged and this handle is no longer "
@@ -327,7 +342,7 @@ int require_mlp(const dppo_handle* h) {
 // -- a 1-rank one too, so the collective path (slab reduce -> ncclAllReduce -> clip + Adam, the
 // advantage-stat all-reduce) runs and is tested on a single GPU -- or a loopback group.
 inline bool distributed(const dppo_handle* h) {
-  return h->comm != nullptr || (h->loop && h->nranks > 1);
+  return h->comm != nullptr || (h->loop && h->nranks > 1) || h->xworld > 0;
 }
 inline int world_of(const dppo_handle* h) { return distributed(h) ? h->nranks : 1; }
 
@@ -390,8 +405,30 @@ int loop_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s)
   return DPPO_OK;
 }
 
+// Exchange numbers: the same sequence on every rank; 0 is skipped (the tagged words start as 0).
+unsigned next_xseq(dppo_handle* h) {
+  if (++h->xseq == 0u) ++h->xseq;
+  return h->xseq;
+}
+
+int peer_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s) {
+  PeerArgs a{};
+  a.src = buf;
+  a.dst = buf;
+  for (int r = 0; r < h->xworld; ++r) a.bufs[r] = h->xpeer[r];
+  a.n = (int64_t)n;
+  a.data_bytes = h->xcap * 8;
+  a.world = h->xworld;
+  a.rank = h->rank;
+  a.seq = next_xseq(h);
+  a.err = h->err_dev;
+  a.timeout_ticks = h->xticks;
+  return launch_peer_sum(a, f64, s);
+}
+
 int allreduce(dppo_handle* h, void* buf, size_t n, ncclDataType_t t, hipStream_t s) {
   if (!distributed(h)) return DPPO_OK;
+  if (h->xworld > 0) return peer_allreduce(h, buf, n, t == ncclFloat64, s);
   if (h->loop) return loop_allreduce(h, buf, n, t == ncclFloat64, s);
   DPPO_NCCL_CHECK(ncclAllReduce(buf, buf, n, t, ncclSum, h->comm, s));
   return DPPO_OK;
@@ -601,14 +638,19 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
       // reduction, [all-reduce], clip + Adam kernel -- on one device, so the N > 1 kernels are
       // checked against the reference traces without a second GPU
       // A device that cannot hold reduce_adam_kernel's grid at once takes the same sequence.
-      const bool multi =
-          distributed(h) || !h->radam_ok || std::getenv("DPPO_SPLIT_ADAM") != nullptr;
+      // Over a peer exchange the cross-rank sum runs inside reduce_adam_kernel (each block
+      // publishes its slice and sums the ranks' slices before the norm), so the multi-rank learn
+      // keeps the single-device sequence: minibatch kernel -> reduce_adam, one launch each.
+      const bool split = std::getenv("DPPO_SPLIT_ADAM") != nullptr;
+      const bool peer = h->xworld > 0 && h->xfused && h->radam_ok && !split;
+      const bool multi = (distributed(h) && !peer) || !h->radam_ok || split;
       if (!multi) {
-        // single device: fused kernel -> slab reduce + clip + Adam in one launch
+        // single device (or peer exchange): fused kernel -> slab reduce + clip + Adam in one launch
         GradArgs ga{};
         ga.params = params;
         ga.rec = h->rec;
         ga.idx = idx;
+        ga.seg = seg;
         ga.m = mb;
         ga.inv_m = inv_m;
         ga.clip_eps = hp->ppo_clip;
@@ -617,8 +659,10 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
         ga.slabs = h->slabs;
         ga.slab_stride = h->slab_stride;
         ga.p_total = h->layout.total;
-        const bool fused_tail = std::getenv("DPPO_FUSED_ADAM") != nullptr;
-        int G = mb_grid(h->sh, mb, fused_tail);
+        const bool fused_tail = std::getenv("DPPO_FUSED_ADAM") != nullptr && !peer;
+        // with `seg` (global minibatches) the share is known only on the device: the handle's
+        // grid, as minibatch_grad
+        int G = seg ? h->G : mb_grid(h->sh, mb, fused_tail);
         if (G > h->G) G = h->G;
         // DPPO_FUSED_ADAM=1: the slab reduction, clip and Adam as the minibatch kernel's own
         // tail (one launch per minibatch, two grid fan-ins).  Measured: the tail costs what
@@ -660,13 +704,26 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
 #else
         const int Gr = G;
 #endif
+        PeerArgs pa{};
+        if (peer) {
+          for (int r = 0; r < h->xworld; ++r) pa.bufs[r] = h->xpeer[r];
+          pa.data_bytes = h->xcap * 8;
+          pa.world = h->xworld;
+          pa.rank = h->rank;
+          pa.seq = next_xseq(h);
+          pa.err = h->err_dev;
+          pa.timeout_ticks = h->xticks;
+        }
+        // a block's intra-device fan-in starts after its peer wait: bound it like the peer wait
+        const unsigned long long fan_ticks =
+            peer && h->xticks > h->fanin_ticks ? h->xticks : h->fanin_ticks;
         DPPO_TRY(launch_reduce_adam(
             h->slabs, Gr, h->slab_stride, h->layout.total, h->grad, h->ra_tags, h->po.ls,
-            d.continuous ? d.act_dim : 0, hp->entropy_beta, d.continuous ? 1 : 0,
-            next_radam_epoch(h), params, adam_m, adam_v, hp->grad_norm_clip, (float)(-step_size),
-            (float)bc2_sqrt,
+            d.continuous ? d.act_dim : 0, hp->entropy_beta,
+            (d.continuous && h->rank == 0) ? 1 : 0, next_radam_epoch(h), params, adam_m,
+            adam_v, hp->grad_norm_clip, (float)(-step_size), (float)bc2_sqrt,
             hp->adam_beta1, hp->adam_beta2, hp->adam_eps, trace, inv_m, hp->value_loss_weight,
-            hp->entropy_beta, h->err_dev, h->fanin_ticks, s));
+            hp->entropy_beta, h->err_dev, fan_ticks, s, peer ? &pa : nullptr));
         continue;
       }
       DPPO_TRY(minibatch_grad(h, params, idx, seg, mb, m_total, hp, s));
@@ -846,6 +903,9 @@ void dppo_destroy(dppo_handle* h) {
     h->loop->break_locked();
   }
   if (h->comm) ncclCommDestroy(h->comm);
+  for (int r = 0; r < kMaxPeers; ++r)
+    if (h->xmapped[r]) (void)hipIpcCloseMemHandle(h->xpeer[r]);
+  if (h->xbuf) (void)hipFree(h->xbuf);
   if (h->loop_out) (void)hipFree(h->loop_out);
   if (h->loop_ready) (void)hipEventDestroy(h->loop_ready);
   if (h->loop_done) (void)hipEventDestroy(h->loop_done);
@@ -1218,6 +1278,182 @@ int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id1
   h->nranks = nranks;
   h->rank = rank;
   return DPPO_OK;
+}
+
+// ---- peer exchange (peer.hip) ---------------------------------------------------------------
+static void peer_unmap(dppo_handle* h) {
+  for (int r = 0; r < kMaxPeers; ++r) {
+    if (h->xmapped[r]) (void)hipIpcCloseMemHandle(h->xpeer[r]);
+    h->xmapped[r] = false;
+    h->xpeer[r] = nullptr;
+  }
+  h->xworld = 0;
+}
+
+int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
+  if (!h || !out64) {
+    set_error("invalid argument to dppo_peer_export");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  if (!h->xbuf) {
+    const int64_t cap = h->layout.total + 8 > 64 ? h->layout.total + 8 : 64;
+    if (cap > (int64_t)kPeerChunk * kPeerMaxSlices) {
+      set_error("peer exchange: %lld parameters exceed the exchange's %d elements",
+                (long long)cap, kPeerChunk * kPeerMaxSlices);
+      return DPPO_EUNSUPPORTED;
+    }
+    // a whole 2 MiB allocation of its own (IPC maps allocations, not sub-ranges of a pool)
+    const int64_t bytes = (peer_buffer_bytes(cap) + (2 << 20) - 1) / (2 << 20) * (2 << 20);
+    DPPO_TRY(dalloc(&h->xbuf, bytes));
+    DPPO_HIP_CHECK(hipMemset(h->xbuf, 0, (size_t)bytes));
+    DPPO_HIP_CHECK(hipDeviceSynchronize());
+    h->xcap = cap;
+  }
+  hipIpcMemHandle_t hd;
+  static_assert(sizeof(hd) == 64, "hipIpcMemHandle_t size");
+  DPPO_HIP_CHECK(hipIpcGetMemHandle(&hd, h->xbuf));
+  std::memcpy(out64, &hd, 64);
+  return DPPO_OK;
+}
+
+int dppo_peer_open(dppo_handle* h, int32_t nranks, int32_t rank, const unsigned char* handles,
+                   int32_t flags) {
+  if (!h || !handles || nranks < 1 || nranks > kMaxPeers || rank < 0 || rank >= nranks) {
+    set_error("invalid argument to dppo_peer_open (1..%d ranks)", kMaxPeers);
+    return DPPO_EINVAL;
+  }
+  if (!h->xbuf || h->xworld > 0 || h->loop) {
+    set_error("dppo_peer_open: needs dppo_peer_export first, no open exchange, no loopback group");
+    return DPPO_EINVAL;
+  }
+  if (h->comm && (nranks != h->nranks || rank != h->rank)) {
+    set_error("dppo_peer_open: rank %d of %d disagrees with the communicator's %d of %d", rank,
+              nranks, h->rank, h->nranks);
+    return DPPO_EINVAL;
+  }
+  if (h->gmb && nranks != h->dims.world_size) {
+    set_error("dppo_peer_open: global_minibatches handle of world_size %d cannot join %d ranks",
+              h->dims.world_size, nranks);
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  for (int r = 0; r < nranks; ++r) {
+    if (r == rank) {
+      h->xpeer[r] = h->xbuf;
+      continue;
+    }
+    hipIpcMemHandle_t hd;
+    std::memcpy(&hd, handles + 64 * r, 64);
+    void* p = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&p, hd, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      peer_unmap(h);
+      set_error("dppo_peer_open: mapping rank %d's exchange buffer failed: %s", r,
+                hipGetErrorString(e));
+      return DPPO_ECOMM;
+    }
+    h->xpeer[r] = (char*)p;
+    h->xmapped[r] = true;
+  }
+  const char* t = std::getenv("DPPO_PEER_TIMEOUT_S");
+  const double sec = t ? std::atof(t) : 60.0;
+  h->xticks = (unsigned long long)((sec > 0.0 ? sec : 60.0) * 1e8);
+  // The fused form needs every rank's reduce_adam grid resident at once: true with one GPU per
+  // rank, not when ranks share a device (their grids would wait on each other for CUs).
+  const char* fz = std::getenv("DPPO_PEER_FUSED");
+  h->xfused = !(flags & DPPO_PEER_SHARED_DEVICE) && !(fz && fz[0] == '0');
+  h->xworld = nranks;
+  h->nranks = nranks;
+  h->rank = rank;
+  return DPPO_OK;
+}
+
+int dppo_peer_close(dppo_handle* h) {
+  if (!h) {
+    set_error("invalid argument to dppo_peer_close");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  DPPO_HIP_CHECK(hipDeviceSynchronize());
+  peer_unmap(h);
+  // a failed exchange (e.g. the self-test) leaves nothing in flight after the synchronisation:
+  // the handle is usable again on its other transport
+  if (h->err_host && __atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) == kErrPeerTimeout)
+    __atomic_store_n(h->err_host, 0u, __ATOMIC_RELEASE);
+  if (!h->comm) {
+    h->nranks = h->dims.world_size;
+    h->rank = h->dims.rank;
+  }
+  return DPPO_OK;
+}
+
+int dppo_peer_allreduce(dppo_handle* h, void* buf, int64_t n, int32_t f64, void* stream) {
+  if (!h || !buf || n < 1) {
+    set_error("invalid argument to dppo_peer_allreduce");
+    return DPPO_EINVAL;
+  }
+  if (h->xworld < 1) {
+    set_error("dppo_peer_allreduce: no open peer exchange (dppo_peer_open)");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(device_status(h));
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  return peer_allreduce(h, buf, (size_t)n, f64 != 0, S(stream));
+}
+
+int dppo_peer_selftest(dppo_handle* h, void* stream) {
+  if (!h || h->xworld < 1) {
+    set_error("dppo_peer_selftest: no open peer exchange (dppo_peer_open)");
+    return DPPO_EINVAL;
+  }
+  DPPO_TRY(device_status(h));
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  hipStream_t s = S(stream);
+  const int W = h->xworld;
+  const int64_t n = h->layout.total + 8;
+  // rank r contributes (r + 1) * (i % 7 + 1) (f32) and (r + 1) * 0.25 (f64): exact sums
+  std::vector<float> hf((size_t)n);
+  for (int64_t i = 0; i < n; ++i) hf[i] = (float)((h->rank + 1) * (int)(i % 7 + 1));
+  double hd[2] = {(h->rank + 1) * 0.25, -(h->rank + 1) * 0.5};
+  float* df = nullptr;
+  double* dd = nullptr;
+  DPPO_TRY(dalloc(&df, n));
+  DPPO_TRY(dalloc(&dd, 2));
+  int rc = DPPO_OK;
+  auto run = [&]() -> int {
+    DPPO_HIP_CHECK(hipMemcpyAsync(df, hf.data(), n * 4, hipMemcpyHostToDevice, s));
+    DPPO_HIP_CHECK(hipMemcpyAsync(dd, hd, 16, hipMemcpyHostToDevice, s));
+    DPPO_TRY(peer_allreduce(h, df, (size_t)n, false, s));
+    DPPO_TRY(peer_allreduce(h, dd, 2, true, s));
+    DPPO_HIP_CHECK(hipMemcpyAsync(hf.data(), df, n * 4, hipMemcpyDeviceToHost, s));
+    DPPO_HIP_CHECK(hipMemcpyAsync(hd, dd, 16, hipMemcpyDeviceToHost, s));
+    DPPO_HIP_CHECK(hipStreamSynchronize(s));
+    DPPO_TRY(device_status(h));
+    const int tri = W * (W + 1) / 2;
+    for (int64_t i = 0; i < n; ++i) {
+      if (hf[i] != (float)(tri * (int)(i % 7 + 1))) {
+        set_error("peer exchange self-test: element %lld is %g, expected %d", (long long)i,
+                  (double)hf[i], tri * (int)(i % 7 + 1));
+        return DPPO_ECOMM;
+      }
+    }
+    if (hd[0] != tri * 0.25 || hd[1] != -tri * 0.5) {
+      set_error("peer exchange self-test: f64 sums %g %g, expected %g %g", hd[0], hd[1],
+                tri * 0.25, -tri * 0.5);
+      return DPPO_ECOMM;
+    }
+    return DPPO_OK;
+  };
+  // a peer that cannot see our buffer fails the test in seconds, not after the learn's bound
+  const unsigned long long ticks = h->xticks;
+  if (h->xticks > 1000000000ull) h->xticks = 1000000000ull;
+  rc = run();
+  h->xticks = ticks;
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(df);
+  (void)hipFree(dd);
+  return rc;
 }
 
 int dppo_loopback_group(dppo_handle** hs, int32_t n) {

@@ -141,6 +141,7 @@ __device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v,
 // mapped), written by kernels with system-scope vector stores and read by the host at the start
 // of the next C-ABI call without any synchronisation (capi.cpp device_status).
 constexpr unsigned kErrFaninTimeout = 1u;  // a grid-wide fan-in gave up waiting: grid not resident
+constexpr unsigned kErrPeerTimeout = 2u;   // a peer exchange gave up waiting for another rank
 // Default bound of one fan-in wait, in s_memrealtime ticks (100 MHz): 5 s.  A resident grid
 // arrives within microseconds; only a grid that is NOT co-resident (another process holding CUs
 // with a long kernel, a partitioned device) can wait this long.
@@ -258,12 +259,16 @@ int launch_clip_adam_traced(float* params, float* grad, float* m, float* v, int6
 // slab reduce + clip + Adam fused (single device): `tags` = reduce_adam_tag_words(p_total)
 // 64-bit words zeroed once; launch number `epoch` (1, 2, ...) publishes and waits for words
 // tagged `epoch`.  On a wait timeout the blocks leave their parameters untouched and set *err.
+struct PeerArgs;
+// `peer` (may be null): sum each block's gradient slice over the ranks of a peer exchange before
+// the norm (peer.hip; src / dst / n unused, seq = this exchange's number)
 int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p_total, float* grad,
                        unsigned long long* tags, int64_t ls_off, int ls_n, float ent_coef,
                        int add_entropy_const, unsigned epoch, float* params,
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
-                       float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s);
+                       float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s,
+                       const PeerArgs* peer = nullptr);
 // Workgroups of reduce_adam_kernel that fit on the device at once (occupancy x CUs; 0 when the
 // layout has more tagged words than the kernel's polling wave holds).
 int reduce_adam_capacity(int device, int64_t p_total);
@@ -279,6 +284,63 @@ int launch_clip_adam(float* params, float* grad, float* m, float* v, int64_t n, 
 // out[i] = src[0][i] + src[1][i] + ... + src[n-1][i] in rank order (f32 or f64 when `f64`); the
 // device-local stand-in for the RCCL sum of a single-device loopback group (capi.cpp)
 constexpr int kMaxLoopRanks = 8;
+
+// Peer exchange (peer.hip): one-shot all-reduce over the ranks' mapped exchange buffers.
+constexpr int kMaxPeers = 8;
+constexpr int kPeerChunk = 1024;      // elements per workgroup (one flag each)
+constexpr int kPeerMaxSlices = 64;    // up to 65,536 elements per exchange
+struct PeerArgs {
+  const void* src;        // this rank's vector (n elements)
+  void* dst;              // the rank-ordered sum (may alias src)
+  char* bufs[kMaxPeers];  // every rank's exchange buffer as mapped in this process
+  int64_t n;
+  int64_t data_bytes;     // bytes of one parity's data region
+  int world, rank;
+  unsigned seq;           // exchange number, the same sequence on every rank (1, 2, ...)
+  unsigned* err;          // the handle's sticky device error word
+  unsigned long long timeout_ticks;
+};
+int64_t peer_buffer_bytes(int64_t cap);  // cap = elements (of up to 8 B) per parity
+int launch_peer_sum(const PeerArgs& a, bool f64, hipStream_t s);
+
+// Exchange buffer of rank r (each region data_bytes = cap x 8 B):
+//   [values, parity 0][values, parity 1][tagged words, parity 0][tagged words, parity 1]
+//   [kPeerMaxSlices slice flags, 64 B apart]
+// Values + slice flags: peer_sum_kernel (any element type).  Tagged words {seq, float}: the
+// gradient exchange inside reduce_adam_kernel, where the data is its own arrival flag.  Data moves
+// with system-scope (sc0 sc1) stores and loads: coherent across GPUs on their own, no L2
+// write-back or invalidate (peer.hip).
+__device__ __forceinline__ unsigned* peer_flag(const PeerArgs& a, int r, int slot) {
+  return (unsigned*)(a.bufs[r] + 4 * a.data_bytes + 64 * (int64_t)slot);
+}
+__device__ __forceinline__ unsigned long long* peer_tagged(const PeerArgs& a, int r) {
+  return (unsigned long long*)(a.bufs[r] + (2 + (int64_t)(a.seq & 1u)) * a.data_bytes);
+}
+template <typename T>
+__device__ __forceinline__ void peer_put(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T peer_get(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Wait until *f reaches a.seq (wrap-safe); false -- with kErrPeerTimeout raised -- after
+// a.timeout_ticks of wall clock or once the handle's error word is already set.
+__device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned k = 0;
+       (int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.seq) < 0; ++k) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((k & 255u) == 255u) {
+      const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
+      if (late || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        __hip_atomic_store(a.err, kErrPeerTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+  }
+  return true;
+}
 struct RankPtrs {
   const void* p[kMaxLoopRanks];
 };

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     unsigned epoch, float* __restrict__ params, float* __restrict__ m,
     float* __restrict__ v, float max_norm, float neg_step_size, float bc2_sqrt, float beta1,
     float beta2, float eps, float* __restrict__ trace, float inv_m, float vf, float ent,
-    unsigned* err, unsigned long long timeout_ticks) {
+    unsigned* err, unsigned long long timeout_ticks, PeerArgs pl) {
 #pragma clang fp contract(off)
   __shared__ float part[kRedWaves][kRedParams];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -194,6 +194,47 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
   RA_EDGE(1);
   if (wave != 0) return;
   if (add_entropy_const && p >= ls_off && p < ls_off + ls_n) t -= ent_coef;
+  if (pl.world > 0) {
+    // data parallel over a peer exchange: publish this block's 64 sums as tagged words {seq,
+    // value} in this rank's buffer (the data is its own arrival flag: one system-scope store, no
+    // drain, no flag round trip), poll word p of every rank until it carries this exchange's
+    // tag, and sum in rank order (the same bits on every rank) -- the cross-rank step of the
+    // minibatch, inside this launch
+    if (p < n) peer_put(peer_tagged(pl, pl.rank) + p, tag_word(pl.seq, t));
+    float x[kMaxPeers];
+    unsigned pend = 0;
+#pragma unroll
+    for (int r = 0; r < kMaxPeers; ++r) {
+      x[r] = 0.f;
+      if (r < pl.world && p < n) pend |= 1u << r;
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned k = 0;; ++k) {
+#pragma unroll
+      for (int r = 0; r < kMaxPeers; ++r) {
+        if (pend & (1u << r)) {
+          const unsigned long long w = peer_get(peer_tagged(pl, r) + p);
+          if ((unsigned)(w >> 32) == pl.seq) {
+            x[r] = __uint_as_float((unsigned)w);
+            pend &= ~(1u << r);
+          }
+        }
+      }
+      if (__ballot(pend != 0) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      if ((k & 255u) == 255u) {
+        const bool late = __builtin_amdgcn_s_memrealtime() - t0 > pl.timeout_ticks;
+        if (late || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+          __hip_atomic_store(err, kErrPeerTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return;  // parameters untouched; the handle reports the error
+        }
+      }
+    }
+    t = x[0];
+#pragma unroll
+    for (int r = 1; r < kMaxPeers; ++r)
+      if (r < pl.world) t += x[r];
+  }
   if (p < n) grad[p] = t;
   double q = (p < p_total) ? (double)t * (double)t : 0.0;
   for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
@@ -344,11 +385,21 @@ int launch_reduce_adam(const float* slabs, int G, int64_t slab_stride, int64_t p
                        int add_entropy_const, unsigned epoch, float* params,
                        float* m, float* v, float max_norm, float neg_step_size, float bc2_sqrt,
                        float beta1, float beta2, float eps, float* trace, float inv_m, float vf,
-                       float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s) {
+                       float ent, unsigned* err, unsigned long long timeout_ticks, hipStream_t s,
+                       const PeerArgs* peer) {
+  PeerArgs pl{};
+  if (peer) {
+    pl = *peer;
+    if ((p_total + 8) * 8 > pl.data_bytes) {
+      set_error("peer exchange: %lld gradient values exceed the exchange buffer",
+                (long long)(p_total + 8));
+      return DPPO_EUNSUPPORTED;
+    }
+  }
   DPPO_LAUNCH(reduce_adam_kernel, dim3(reduce_adam_blocks(p_total)), dim3(kRedThreads), 0, s, slabs, G,
               slab_stride, p_total, grad, tags, ls_off, ls_n, ent_coef, add_entropy_const,
               epoch, params, m, v, max_norm, neg_step_size, bc2_sqrt, beta1, beta2, eps,
-              trace, inv_m, vf, ent, err, timeout_ticks);
+              trace, inv_m, vf, ent, err, timeout_ticks, pl);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

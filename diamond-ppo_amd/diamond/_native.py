@@ -33,6 +33,8 @@ EXPORTED = [
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
     "dppo_perm_targets_numpy", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
+    "dppo_peer_export", "dppo_peer_open", "dppo_peer_close", "dppo_peer_allreduce",
+    "dppo_peer_selftest",
     "dppo_gru_param_layout", "dppo_gru_create", "dppo_gru_destroy", "dppo_gru_minibatch_grad_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
@@ -138,6 +140,11 @@ def load():
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
         "dppo_loopback_group": (ctypes.c_int, [P(vp), i32]),
+        "dppo_peer_export": (ctypes.c_int, [vp, vp]),
+        "dppo_peer_open": (ctypes.c_int, [vp, i32, i32, vp, i32]),
+        "dppo_peer_close": (ctypes.c_int, [vp]),
+        "dppo_peer_allreduce": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+        "dppo_peer_selftest": (ctypes.c_int, [vp, vp]),
         "dppo_status": (ctypes.c_int, [vp]),
         "dppo_actor_forward_f32": (ctypes.c_int, [vp, vp, vp, i64, vp, vp]),
         "dppo_fanin_selftest": (ctypes.c_int, [vp, i32, i32, i64, vp]),
@@ -320,6 +327,32 @@ class Handle:
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         buf = ctypes.create_string_buffer(uid, 128)
         check(self.lib.dppo_comm_init(self.h, int(nranks), int(rank), buf), "dppo_comm_init")
+
+    # peer exchange (csrc/peer.hip): one-shot all-reduce over the ranks' mapped buffers
+    def peer_export(self) -> bytes:
+        buf = ctypes.create_string_buffer(64)
+        check(self.lib.dppo_peer_export(self.h, buf), "dppo_peer_export")
+        return buf.raw
+
+    def peer_open(self, nranks: int, rank: int, handles: bytes, shared_device=False) -> str:
+        """Map every rank's exchange buffer; returns "" or the error text (no exception: the
+        ranks must agree on the outcome before any of them exchanges).  shared_device: some
+        ranks run on the same GPU (DPPO_PEER_SHARED_DEVICE)."""
+        buf = ctypes.create_string_buffer(bytes(handles), 64 * int(nranks))
+        rc = self.lib.dppo_peer_open(self.h, int(nranks), int(rank), buf,
+                                     1 if shared_device else 0)
+        return "" if rc == 0 else (self.lib.dppo_last_error().decode() or f"rc {rc}")
+
+    def peer_selftest(self, stream) -> str:
+        rc = self.lib.dppo_peer_selftest(self.h, stream)
+        return "" if rc == 0 else (self.lib.dppo_last_error().decode() or f"rc {rc}")
+
+    def peer_close(self):
+        check(self.lib.dppo_peer_close(self.h), "dppo_peer_close")
+
+    def peer_allreduce(self, ptr: int, n: int, f64: bool, stream):
+        check(self.lib.dppo_peer_allreduce(self.h, ptr, int(n), int(bool(f64)), stream),
+              "dppo_peer_allreduce")
 
 
 class GruHandle:

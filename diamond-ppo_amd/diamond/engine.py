@@ -29,7 +29,9 @@ from __future__ import annotations
 import collections
 import ctypes
 import os
+import socket
 import threading
+import warnings
 import time
 from dataclasses import dataclass
 
@@ -393,13 +395,33 @@ class NativeLearner:
         self._closed = False
 
     def _init_comm(self):
+        """The rank exchange of the data-parallel learn.  DPPO_COMM: "auto" (default) = an RCCL
+        communicator plus, for 2-8 ranks, the peer exchange (csrc/peer.hip: one-shot all-reduce
+        over the ranks' xGMI-mapped buffers) when every rank maps every buffer and passes its
+        self-test -- otherwise RCCL carries the exchange; "rccl" = RCCL only; "peer" = the peer
+        exchange only (no communicator; also how two ranks share one GPU in the tests)."""
         d = torch.distributed
+        self.peer = False
+        mode = os.environ.get("DPPO_COMM", "auto")
+        if mode not in ("auto", "rccl", "peer"):
+            raise ValueError(f"DPPO_COMM={mode!r}: expected auto, rccl or peer")
         if not (d.is_available() and d.is_initialized()):   # one rank, no process group
-            self.handle.comm_init(1, 0, N.comm_unique_id())
+            if mode == "peer":   # (DPPO_FORCE_COMM=1: the 1-rank exchange, measurements)
+                h = self.handle
+                err = h.peer_open(1, 0, h.peer_export()) or h.peer_selftest(
+                    torch.cuda.current_stream(self.device).cuda_stream)
+                if err:
+                    raise RuntimeError(f"peer exchange unavailable: {err}")
+                self.peer = True
+            else:
+                self.handle.comm_init(1, 0, N.comm_unique_id())
             return
-        obj = [N.comm_unique_id() if self.rank == 0 else None]
-        d.broadcast_object_list(obj, src=0)
-        self.handle.comm_init(self.world, self.rank, obj[0])
+        if mode != "peer":
+            obj = [N.comm_unique_id() if self.rank == 0 else None]
+            d.broadcast_object_list(obj, src=0)
+            self.handle.comm_init(self.world, self.rank, obj[0])
+        if mode == "peer" or (mode == "auto" and 1 < self.world <= 8):
+            self.peer = self._init_peer(d, required=mode == "peer")
         # replicate rank 0's initial parameters (identical seeds make this a no-op in practice)
         if d.get_backend() == "nccl":
             d.broadcast(self.flat.flat, src=0)
@@ -407,6 +429,37 @@ class NativeLearner:
             cpu = self.flat.flat.cpu()
             d.broadcast(cpu, src=0)
             self.flat.flat.copy_(cpu)
+
+    def _all_ranks(self, d, ok: bool) -> bool:
+        dev = self.device if d.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        d.all_reduce(t, op=d.ReduceOp.MIN)
+        return bool(t.item())
+
+    def _init_peer(self, d, required: bool) -> bool:
+        """Map every rank's exchange buffer and run one checked exchange; every rank keeps the
+        peer exchange only if every rank succeeded (ranks must never disagree on the transport)."""
+        h = self.handle
+        pr = torch.cuda.get_device_properties(self.device)
+        me = (h.peer_export(), (socket.gethostname(), pr.pci_domain_id, pr.pci_bus_id,
+                                pr.pci_device_id))
+        mine = [None] * self.world
+        d.all_gather_object(mine, me)
+        gpus = [m[1] for m in mine]
+        err = h.peer_open(self.world, self.rank, b"".join(m[0] for m in mine),
+                          shared_device=len(set(gpus)) < len(gpus))
+        if self._all_ranks(d, not err):
+            err = h.peer_selftest(torch.cuda.current_stream(self.device).cuda_stream)
+            if self._all_ranks(d, not err):
+                return True
+            h.peer_close()
+        elif not err:
+            h.peer_close()
+        msg = f"peer exchange unavailable on rank {self.rank}: {err or 'another rank failed'}"
+        if required:
+            raise RuntimeError(msg)
+        warnings.warn(msg + "; RCCL carries the exchange")
+        return False
 
     # -----------------------------------------------------------------------------------------
     def act(self, observations: np.ndarray, seed: int, squash=None):

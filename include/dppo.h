@@ -283,6 +283,32 @@ int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t
 int dppo_comm_unique_id(char* out128);
 int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id128);
 
+/* Peer exchange (single node, all GPUs directly linked over xGMI): a one-shot all-reduce that
+ * replaces the RCCL calls above.  Every rank exports its exchange buffer (64-byte IPC handle),
+ * the caller all-gathers the handles (e.g. torch.distributed.all_gather_object) and every rank
+ * opens all of them; from then on each all-reduce of dppo_learn_f32 is one kernel that publishes
+ * the rank's vector in its own buffer and sums all ranks' buffers in rank order (the same bits on
+ * every rank).  Works with or without a communicator (dppo_comm_init); ranks must agree on using
+ * it (run dppo_peer_selftest on every rank, agree on the results, dppo_peer_close on failure).
+ * Waits are bounded by DPPO_PEER_TIMEOUT_S (default 60 s); a timeout makes dppo_status return
+ * DPPO_ECOMM.  No reference counterpart (the reference is single-process); replaces the
+ * torch.distributed all-reduce a data-parallel wrapper of ppo.py:276-285 would issue. */
+int dppo_peer_export(dppo_handle* h, unsigned char* out64);
+#define DPPO_PEER_SHARED_DEVICE 1 /* flags: some ranks share a GPU (keeps the exchange a kernel of
+                                    its own instead of fusing it into the optimizer step, whose
+                                    grids could not all be resident) */
+int dppo_peer_open(dppo_handle* h, int32_t nranks, int32_t rank, const unsigned char* handles,
+                   int32_t flags);
+int dppo_peer_close(dppo_handle* h);
+/* The gradient exchange of each minibatch runs inside the optimizer-step kernel (each block
+ * publishes its 64 gradient sums, waits for the same block of every rank, sums in rank order,
+ * then the norm and Adam as on one device): one launch after the minibatch kernel, as on one GPU.
+ * The advantage statistics use the stand-alone exchange kernel.
+ * every rank's `n` values summed in rank order into buf, in place (f64 != 0: doubles) */
+int dppo_peer_allreduce(dppo_handle* h, void* buf, int64_t n, int32_t f64, void* stream);
+/* one exchange of a known pattern (f32 and f64) checked exactly; synchronous */
+int dppo_peer_selftest(dppo_handle* h, void* stream);
+
 /* Sticky device-side error of the handle, read WITHOUT synchronising (host-coherent word the
  * kernels write): DPPO_EHIP once a grid-wide fan-in of the single-device optimizer step timed
  * out (its workgroups were not all resident at once -- another process holding the CUs, a

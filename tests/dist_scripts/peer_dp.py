@@ -1,0 +1,149 @@
+"""One rank of a `world`-process job on ONE GPU whose ranks exchange through the peer exchange
+(csrc/peer.hip: every rank's buffer mapped into every other rank over IPC, one-shot all-reduce),
+for tests/test_gpu_peer.py.  RCCL refuses two ranks on one device, so this is how the peer path
+runs on a one-GPU box; on a node the same code maps the buffers over xGMI.
+
+kind "handle": the C ABI directly -- the exchange self-test, the latency of one gradient-sized
+exchange, then dppo_learn_f32 on this rank's env shard in both minibatch modes, against the
+world-1 learn of the global buffer (rank 0 runs it).  kind "agent": the drop-in PPO under
+DPPO_COMM=peer (engine._init_comm maps, self-tests and agrees), one learn per rank.
+Results go to `out_path` (npz).  Test infrastructure only."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+
+def _paths():
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    for p in (os.path.join(root, "diamond-ppo_amd"), root, os.path.join(root, "tests"),
+              os.path.join(root, "tests", "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _global_setup(T, Ng, D, A, cont, E, M, seed):
+    from diamond import _native as N
+    from gpu_helpers import H, random_params, synth
+    from oracle import ppo_np as P
+    L = N.param_layout(N.Dims(T, Ng, D, A, int(cont), H, E, M, 1, 0))
+    names = P.CONTINUOUS_NAMES if cont else P.DISCRETE_NAMES
+    params, flat0 = random_params(L, names, D, A, cont, np.random.default_rng(seed))
+    _, host = synth(T, Ng, D, A, cont, seed)
+    host = tuple(x if x.dtype != np.uint8 else x.astype(bool) for x in host)
+    return flat0, host
+
+
+def _learn(h, host, lo, hi, flat0, perms, cont):
+    import torch
+    import diamond
+    from gpu_helpers import dev, hparams, stream
+    from diamond import _native as N
+    obs, nobs, act, rew, te, tr = host
+    exp = [[obs[k, lo:hi], nobs[k, lo:hi], act[k, lo:hi], rew[k, lo:hi], te[k, lo:hi],
+            tr[k, lo:hi]] for k in range(obs.shape[0])]
+    ro = diamond.engine.stage_experience(exp, dev(), cont)
+    p = torch.from_numpy(flat0).to(dev())
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    hp = hparams()
+    pg = np.ascontiguousarray(perms, dtype=np.int32)
+    N.check(h.lib.dppo_learn_f32(h.h, ctypes.byref(ro.as_struct()), p.data_ptr(), m.data_ptr(),
+                                 v.data_ptr(), ctypes.byref(hp), pg.ctypes.data, None, stream()))
+    torch.cuda.synchronize()
+    return p.cpu().numpy()
+
+
+def run_handle(rank, world, out):
+    import torch
+    import torch.distributed as dist
+    from diamond import _native as N
+    from gpu_helpers import H, stream
+    T, Nl, D, A, E, M = 16, 32, 4, 2, 4, 8
+    Ng, B = Nl * world, T * Nl
+    res = {}
+    for gmb in (0, 1):
+        h = N.Handle(0, N.Dims(T, Nl, D, A, 0, H, E, M, world, rank, gmb))
+        handles = [None] * world
+        dist.all_gather_object(handles, h.peer_export())
+        err = h.peer_open(world, rank, b"".join(handles), shared_device=True)
+        assert not err, err
+        err = h.peer_selftest(stream())
+        assert not err, err
+        if gmb == 0:
+            # latency of one gradient-sized exchange (P + 8 floats), 200 back to back
+            n = h.layout.total + 8
+            x = torch.zeros(n, device="cuda:0")   # stays 0 through 201 sums
+            dist.barrier()
+            h.peer_allreduce(x.data_ptr(), n, False, stream())
+            torch.cuda.synchronize()
+            dist.barrier()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(200):
+                h.peer_allreduce(x.data_ptr(), n, False, stream())
+            b.record()
+            torch.cuda.synchronize()
+            res["us_per_exchange"] = a.elapsed_time(b) * 1e3 / 200
+            assert float(x.abs().max().item()) == 0.0
+        flat0, host = _global_setup(T, Ng, D, A, False, E, M, seed=11)
+        if gmb:
+            rs = np.random.RandomState(42)
+            perms = np.stack([rs.permutation(B * world) for _ in range(E)]).astype(np.int32)
+            perms_g = perms
+        else:
+            perms_all = [np.stack([np.random.RandomState(100 + r).permutation(B)
+                                   for _ in range(E)]).astype(np.int32) for r in range(world)]
+            perms = perms_all[rank]
+            mb = B // M
+            to_g = lambda r, i: (i // Nl) * Ng + r * Nl + i % Nl
+            perms_g = np.stack([np.concatenate([to_g(r, perms_all[r][e, j * mb:(j + 1) * mb])
+                                                for j in range(M) for r in range(world)])
+                                for e in range(E)])
+        dist.barrier()
+        res[f"params{gmb}"] = _learn(h, host, rank * Nl, (rank + 1) * Nl, flat0, perms, False)
+        res[f"trace{gmb}"] = h.trace(E * M)
+        h.close()
+        if rank == 0:
+            hs = N.Handle(0, N.Dims(T, Ng, D, A, 0, H, E, M, 1, 0))
+            res[f"single{gmb}"] = _learn(hs, host, 0, Ng, flat0, perms_g, False)
+            res[f"single_trace{gmb}"] = hs.trace(E * M)
+            hs.close()
+    np.savez(out, **res)
+
+
+def run_agent(rank, world, out):
+    import torch
+    import diamond
+    import bench
+    from gpu_helpers import SpecEnvs
+    T, Nl, D, A = 32, 64, 4, 2
+    cfg = diamond.PPOConfig(rollout_steps=T, num_envs=Nl, verbose=False)
+    agent = diamond.PPO(None, cfg, envs=SpecEnvs(D, A, False))
+    L = agent._learner
+    assert L.world == world and L.peer, (L.world, getattr(L, "peer", None))
+    init = L.flat.flat.cpu().numpy()
+    ro, _ = bench.synth_rollout(T, Nl, D, A, False, 0.02, 0.005, rank, agent.device)
+    agent.learn_device(ro)
+    torch.cuda.synchronize()
+    np.savez(out, init=init, final=L.flat.flat.cpu().numpy(), trace=agent.learn_trace())
+    L.close()
+
+
+def run(rank, world, port, kind, out):
+    _paths()
+    os.environ["LOCAL_RANK"] = "0"          # every rank on the one GPU
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
+    os.environ["DPPO_COMM"] = "peer"
+    os.environ["DPPO_PEER_TIMEOUT_S"] = "30"
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        (run_handle if kind == "handle" else run_agent)(rank, world, out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,110 @@
+"""The peer exchange (csrc/peer.hip): the data-parallel learn's all-reduces as one
+kernel per exchange that publishes each rank's vector in its own IPC-exported buffer and sums all
+ranks' buffers in rank order.  Two processes share the one GPU of the box (RCCL refuses that; the
+peer exchange does not care whether a mapped buffer is on this device or across xGMI), each
+driving its own handle (tests/dist_scripts/peer_dp.py):
+
+* the C ABI: exact self-test (f32 and f64), then dppo_learn_f32 on each rank's env shard in both
+  minibatch modes -- identical parameters on both ranks, equal to the world-1 learn of the global
+  buffer (local mode: with the union permutations) to the re-association tolerance of
+  test_gpu_dataparallel.py;
+* the drop-in PPO under DPPO_COMM=peer: engine._init_comm maps, self-tests and agrees; one learn
+  leaves both ranks with identical parameters."""
+import multiprocessing as mp
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(kind, tmp_path, world=2):
+    from dist_scripts import peer_dp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    outs = [str(tmp_path / f"{kind}_r{r}.npz") for r in range(world)]
+    procs = [ctx.Process(target=peer_dp.run, args=(r, world, port, kind, outs[r]))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(200)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return [np.load(o) for o in outs]
+
+
+@pytest.mark.timeout(300)
+def test_peer_exchange_two_ranks_learn_matches_single_gpu(tmp_path):
+    r0, r1 = _spawn("handle", tmp_path)
+    print(f"peer exchange, 2 ranks on one GPU: {float(r0['us_per_exchange']):.2f} us per "
+          f"gradient-sized exchange (rank 1: {float(r1['us_per_exchange']):.2f})")
+    for gmb in (0, 1):
+        assert np.array_equal(r0[f"params{gmb}"], r1[f"params{gmb}"]), gmb
+        np.testing.assert_allclose(r0[f"trace{gmb}"][:, 0], r0[f"single_trace{gmb}"][:, 0],
+                                   rtol=2e-5, atol=2e-6, err_msg=f"loss, gmb={gmb}")
+        np.testing.assert_allclose(r0[f"trace{gmb}"][:, 4], r0[f"single_trace{gmb}"][:, 4],
+                                   rtol=2e-5, atol=2e-6, err_msg=f"grad norm, gmb={gmb}")
+        np.testing.assert_allclose(r0[f"params{gmb}"], r0[f"single{gmb}"], rtol=0, atol=5e-6,
+                                   err_msg=f"params, gmb={gmb}")
+
+
+@pytest.mark.timeout(300)
+def test_peer_exchange_drop_in_agent(tmp_path):
+    r0, r1 = _spawn("agent", tmp_path)
+    assert np.array_equal(r0["init"], r1["init"])
+    assert np.array_equal(r0["final"], r1["final"])
+    assert np.all(np.isfinite(r0["final"])) and np.abs(r0["final"] - r0["init"]).max() > 1e-5
+    assert np.array_equal(r0["trace"], r1["trace"])
+
+
+def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces():
+    """A 1-rank peer exchange in this process: every learn() then takes the multi-rank sequence
+    of a node with one GPU per rank -- the advantage statistics through the exchange kernel, and
+    each minibatch's gradient exchange INSIDE reduce_adam_kernel (publish the block's slice, wait
+    for every rank's flag, sum in rank order) -- and must reproduce the reference's captured
+    traces.  (Two ranks sharing this GPU take the unfused exchange: their optimizer-step grids
+    could not be resident at once; the test above.)"""
+    import diamond
+    from conftest import load_golden
+    from gpu_helpers import stream
+    from test_gpu_parity import experience, make_agent
+    for name in ("cartpole_small", "cheetah_small"):
+        z = load_golden(f"learn_{name}.npz")
+        T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
+        agent = make_agent(z)
+        L = agent._learner
+        h = L.handle
+        assert not h.peer_open(1, 0, h.peer_export())
+        assert not h.peer_selftest(stream())
+        h.set_timing(True)
+        losses, norms = [], []
+        for li in range(n_learn):
+            np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
+                                 int(z[f"rng_pos_before{li}"]), 0, 0.0))
+            ro = diamond.engine.stage_experience(experience(z, li), agent.device, bool(cont))
+            agent.learn_device(ro)
+            tr = agent.learn_trace()
+            losses += list(tr[:, 0])
+            norms += list(tr[:, 4])
+        import torch
+        torch.cuda.synchronize()
+        tm = h.timing()
+        E, M = int(z["cfg/num_epochs"]), int(z["cfg/num_minibatches"])
+        assert tm["allreduce"][1] == n_learn, tm                 # advantage statistics only
+        assert tm["reduce_adam"][1] == n_learn * E * M and tm["clip_adam"][1] == 0, tm
+        np.testing.assert_allclose(losses, z["loss"], rtol=2e-5, atol=2e-5, err_msg=name)
+        np.testing.assert_allclose(norms, z["norm"], rtol=2e-5, atol=2e-5, err_msg=name)
+        for n, p in agent.network.named_parameters():
+            np.testing.assert_allclose(p.detach().cpu().numpy(), z["final/" + n], rtol=0,
+                                       atol=5e-6, err_msg=f"{name} {n}")
+        L.close()
