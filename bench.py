@@ -272,7 +272,8 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
             dist.barrier()
         el = time.perf_counter() - t0
         if dist is not None:
-            t = torch.tensor([el], dtype=torch.float64, device=device)
+            t = torch.tensor([el], dtype=torch.float64,
+                             device=device if dist.get_backend() == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el
@@ -382,12 +383,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DPPO_BENCH_REHEARSE=1: rehearse the N > 1 path on a one-GPU box -- every rank on GPU 0, a
+    # gloo process group, the peer exchange between the ranks (RCCL refuses two ranks on one
+    # device).  The numbers then measure ranks sharing one GPU, not scaling.
+    rehearse = world > 1 and os.environ.get("DPPO_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
+        os.environ["LOCAL_RANK"] = "0"   # the agents pick their device from LOCAL_RANK
+        os.environ["DPPO_COMM"] = "peer"
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     main_res = run_config(args.config, world, rank, dist, device, args.steps, args.warmup,
                           kernel_timing=not args.no_kernel_timing,

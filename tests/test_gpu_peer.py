@@ -108,3 +108,26 @@ def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces():
             np.testing.assert_allclose(p.detach().cpu().numpy(), z["final/" + n], rtol=0,
                                        atol=5e-6, err_msg=f"{name} {n}")
         L.close()
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_rank_rehearsal_line():
+    """bench.py's N > 1 path (torch.distributed.run, barrier + max-over-ranks timing, one JSON
+    line from rank 0) rehearsed on the box's one GPU: DPPO_BENCH_REHEARSE=1 puts both ranks on
+    GPU 0 with a gloo group and the peer exchange between them."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, DPPO_BENCH_REHEARSE="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2",
+           "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
+    assert d["config"]["exchange"] == "peer" and d["config"]["num_envs_total"] == 2 * 4096
+    assert d["kernels"]["allreduce"]["launches"] > 0
