@@ -5,6 +5,7 @@
 #    WRITE_SIZE) -- counters never combined with tracing domains;
 #  * GAE alone (tools/gae_bench.py) at N = 8192 and 65,536, both modes: kernel trace + HBM bytes.
 # Output: gpurun_out/prof3/<name>/...; summarise with tools/prof_summary.py.
+# CONFIGS / GAES (|-separated, empty = none) select the runs.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof3
@@ -30,7 +31,9 @@ for C in $CONFIGS; do
     -o p4 -- python3 $B --steps 2 --warmup 1 > $D/pmc4.log 2>&1 || exit 1
   echo "$C done"
 done
-for G in "8192" "8192 --affine" "65536 --sets 3" "65536 --sets 3 --affine"; do
+GAES=${GAES-"8192|8192 --affine|65536 --sets 3|65536 --sets 3 --affine"}
+IFS='|' read -ra GLIST <<< "$GAES"
+for G in "${GLIST[@]}"; do
   set -- $G
   D=$OUT/gae$1$(echo "$G" | grep -q affine && echo _affine)
   mkdir -p $D
