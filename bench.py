@@ -89,7 +89,11 @@ def flops_per_sample(D, A):
     return 2 * F, 2 * V, 2 * (3 * F - D * H)
 
 
-def synth_rollout(T, N, D, A, continuous, p_term, p_trunc, seed, device):
+def synth_rollout(T, N, D, A, continuous, p_term, p_trunc, seed, device, chained=True):
+    """A synthetic [T, N] rollout.  chained (default): the reference rollout's invariant
+    (ppo.py:163-179) -- obs[t+1] is the array env.step returned as next_obs[t], except for the envs
+    that terminated or truncated at t, which were reset to a fresh observation.  chained=False:
+    obs and next_obs drawn independently (no step continues another)."""
     from diamond.engine import DeviceRollout
     rng = np.random.default_rng(seed)
     obs = rng.standard_normal((T, N, D), dtype=np.float32)
@@ -101,6 +105,9 @@ def synth_rollout(T, N, D, A, continuous, p_term, p_trunc, seed, device):
     rew = rng.normal(1.0, 1.0, (T, N)).astype(np.float32)
     te = (rng.random((T, N)) < p_term).astype(np.uint8)
     tr = (rng.random((T, N)) < p_trunc).astype(np.uint8)
+    if chained:
+        done = (te | tr).astype(bool)
+        obs[1:] = np.where(done[:-1, :, None], obs[1:], nobs[:-1])
     g = lambda x: torch.from_numpy(x).to(device)
     return DeviceRollout(g(obs), g(nobs), g(act), g(rew), g(te), g(tr)), (obs, nobs, act, rew, te, tr)
 
@@ -284,6 +291,14 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
                                                                       "draft_start", "draw",
                                                                       "slot_wait")}
     hits = hs["lookahead_hits"]
+    # Pass A' (reported beside it): the same learns on a rollout whose next_obs never continues
+    # into obs -- the old-policy evaluation's next-value reuse (mlp.hip) then finds nothing to
+    # reuse and runs the full critic pass on next_obs
+    ro_chained = ro
+    ro, _ = synth_rollout(T, N, D, A, cont, pt, ptr, seed=rank, device=device, chained=False)
+    agent.learn_device(ro)
+    elapsed_unchained = timed_pass(False)
+    ro = ro_chained
     # Pass B (the per-kernel table and the roofline): the same K learns with the kernels' own
     # start/end HIP events (libdppo timing mode); never the throughput.
     timing = {k: (0.0, 0) for k in NN.TIMING_CLASSES}
@@ -331,6 +346,7 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "value": round(B_global * steps / elapsed, 1),
         "ms_per_step": round(elapsed / steps * 1e3, 4),
         "update_steps_per_s": round(E * M * steps / elapsed, 1),
+        "value_unchained_obs": round(B_global * steps / elapsed_unchained, 1),
         "scaling": scaling,
         "config": {"workload": f"{model}: learn() = old-policy eval + GAE + adv-norm + "
                                f"{E}x{M} minibatch Adam steps", "name": name,
@@ -419,6 +435,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
+            "data_note": "random observations/rewards/dones in the reference rollout's layout: "
+                         "obs[t+1] is next_obs[t] unless that env was reset (ppo.py:163-179); "
+                         "value_unchained_obs: the same learns with independent next_obs",
         }
         out.update({k: v for k, v in main_res.items() if k not in out})
         out["device"] = {"name": torch.cuda.get_device_name(device),

@@ -108,6 +108,9 @@ struct dppo_handle {
         *ret = nullptr, *adv_n = nullptr, *rec = nullptr, *slabs = nullptr, *grad = nullptr,
         *trace = nullptr, *mean_std = nullptr;
   double *partials = nullptr, *dsum = nullptr, *sq_part = nullptr;
+  // next-value reuse of the old-policy evaluation (mlp.hip, EvalReuse)
+  EvalReuse reuse{};
+  bool reuse_on = false;
   unsigned* arrivals = nullptr;  // [4][kArrivalWords]: (unused), fused tail x 2, probe
   unsigned long long* ra_tags = nullptr;  // reduce_adam_kernel's tagged partials (optim.hip)
   // sticky device error word (grid_fanin timeouts): host-coherent pinned memory and its device
@@ -447,7 +450,7 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
   {
     Timed tm(h, K_EVAL, s);
     DPPO_TRY(launch_eval(h->sh, h->po, params, ro->obs, ro->actions, ro->next_obs, h->logp,
-                         h->values, h->next_values, h->B, s));
+                         h->values, h->next_values, h->B, s, h->reuse_on ? &h->reuse : nullptr));
   }
   // (3) GAE + returns (ppo.py:240-241)
   {
@@ -829,6 +832,17 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   chk(dalloc(&h->sq_part, slab_reduce_blocks(h->layout.total)));
   chk(dalloc(&h->arrivals, 4 * kArrivalWords));
   chk(dalloc(&h->ra_tags, reduce_adam_tag_words(h->layout.total)));
+  {
+    // DPPO_EVAL_REUSE=0: the full next_obs critic pass (A/B runs)
+    const char* e = std::getenv("DPPO_EVAL_REUSE");
+    h->reuse_on = dims->rollout_steps >= 2 && !(e && e[0] == '0');
+    if (h->reuse_on) {
+      chk(dalloc(&h->reuse.match, h->B));
+      chk(dalloc(&h->reuse.list, h->B));
+      chk(dalloc(&h->reuse.list_ctr, 2));
+      h->reuse.row = dims->num_envs;
+    }
+  }
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->pe));
     chk(dalloc(&h->targets_dev2[k], E * h->pe));
@@ -881,6 +895,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
     (void)hipMemset(h->arrivals, 0, 4 * kArrivalWords * sizeof(unsigned));
     (void)hipMemset(h->ra_tags, 0, reduce_adam_tag_words(h->layout.total) * sizeof(uint64_t));
+    if (h->reuse_on) (void)hipMemset(h->reuse.list_ctr, 0, 2 * sizeof(unsigned));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }
@@ -923,6 +938,9 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->partials);
   (void)hipFree(h->dsum);
   (void)hipFree(h->sq_part);
+  (void)hipFree(h->reuse.match);
+  (void)hipFree(h->reuse.list);
+  (void)hipFree(h->reuse.list_ctr);
   (void)hipFree(h->arrivals);
   (void)hipFree(h->ra_tags);
   for (int k = 0; k < 2; ++k) {

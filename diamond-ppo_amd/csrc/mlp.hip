@@ -58,6 +58,12 @@ struct KArgs {
   int64_t n;
   // shapes
   int D, D8, nq1, A, R;
+  // next-value reuse (EvalReuse): row > 0 = the buffers are a [T][row] rollout
+  int64_t row;
+  uint8_t* match;
+  int32_t* list;
+  unsigned* list_ctr;
+  int par;
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
@@ -334,6 +340,36 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
         }
       logp = za - (mx + logf(se));
     }
+    if (a.row > 0) {
+      // next_obs[i] bitwise equal to obs[i + row] (the reference's rollout stores the same array
+      // for both unless the env was reset, ppo.py:163-179): V(next_obs[i]) is values[i + row],
+      // computed by this kernel's obs pass with the same instructions -- the same bits.  The
+      // other samples are queued for next_eval_kernel's critic pass.
+      bool need = false;
+      if (valid && h == 0) {
+        bool m = i + a.row < a.n;
+        if (m) {
+          const uint32_t* p = (const uint32_t*)(a.next_obs + ic * a.D);
+          const uint32_t* o = (const uint32_t*)(a.obs + (ic + a.row) * a.D);
+          for (int f = 0; f < a.D; ++f) m = m && p[f] == o[f];
+        }
+        a.match[i] = m ? 1 : 0;
+        need = !m;
+      }
+      const uint64_t bal = __ballot(need);
+      if (bal != 0) {
+        const int first = __builtin_ctzll(bal);
+        unsigned base = 0;
+        if (lane == first) base = atomicAdd(a.list_ctr + a.par, (unsigned)__popcll(bal));
+        base = __shfl(base, first);
+        if (need) a.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)i;
+      }
+      if (valid && h == 0) {
+        a.logp[i] = logp;
+        a.values[i] = v;
+      }
+      continue;
+    }
     // ---- next_obs: base + critic only (get_values, ppo.py:84-89)
     x[0] = load_x0_obs(a.next_obs + ic * a.D, a.D, a.nq1, valid, h);
     dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
@@ -345,6 +381,42 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       a.values[i] = v;
       a.next_values[i] = nv;
     }
+  }
+}
+
+// The critic pass on next_obs for the samples eval_kernel queued (reuse mode), and the reused
+// next values of the others: next_values[i] = values[i + row] where match[i].  Zeroes the other
+// list counter for the next eval launch (which appends to it; the last reader of that counter was
+// the previous launch of this kernel).
+__global__ __launch_bounds__(kThreads, 4) void next_eval_kernel(KArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds_[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + tid; i < a.n;
+       i += (int64_t)gridDim.x * kThreads)
+    if (a.match[i]) a.next_values[i] = a.values[i + a.row];
+  const unsigned cnt = __hip_atomic_load(a.list_ctr + a.par, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && tid == 0) a.list_ctr[a.par ^ 1] = 0u;
+  const int64_t ntiles = ((int64_t)cnt + 31) / 32;
+  if ((int64_t)blockIdx.x * kWaves >= ntiles) return;  // no tile for this workgroup
+  load_weights(lds_, a, tid);
+  __syncthreads();
+  const LdsLayout& L = a.L;
+  const float bv = lds_[L.bv];
+  for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles;
+       tile += (int64_t)gridDim.x * kWaves) {
+    float* lds = opaque_base(lds_);
+    const int64_t k = tile * 32 + l31;
+    const bool valid = k < (int64_t)cnt;
+    const int64_t i = valid ? a.list[k] : 0;
+    f32x16 x[2], y[2];
+    x[0] = load_x0_obs(a.next_obs + i * a.D, a.D, a.nq1, valid, h);
+    dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
+    dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);
+    dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);
+    const float nv = value_head(lds + L.Wv, bv, y, h);
+    if (valid && h == 0) a.next_values[i] = nv;
   }
 }
 
@@ -555,6 +627,8 @@ void raise_lds_limits() {
   DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
   DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
 #undef DPPO_SET
+  (void)hipFuncSetAttribute((const void*)next_eval_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
 #define DPPO_SET(A, C)                                                                  \
   (void)hipFuncSetAttribute((const void*)act_kernel<A, C>,                              \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
@@ -584,9 +658,17 @@ size_t mlp_lds_bytes_eval(const MlpShape& sh) {
 
 int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                 const void* actions, const float* next_obs, float* logp, float* values,
-                float* next_values, int64_t n, hipStream_t s) {
+                float* next_values, int64_t n, hipStream_t s, EvalReuse* reuse) {
   if (n <= 0) return DPPO_OK;
   KArgs k = base_args(sh, po, params);
+  if (reuse && reuse->row > 0 && reuse->row < n) {
+    k.row = reuse->row;
+    k.match = reuse->match;
+    k.list = reuse->list;
+    k.list_ctr = reuse->list_ctr;
+    k.par = reuse->par;
+    reuse->par ^= 1;
+  }
   k.obs = obs;
   k.actions = actions;
   k.next_obs = next_obs;
@@ -610,6 +692,10 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
   if (g > 2 * cus) g = 2 * cus;
   DPPO_DISPATCH(eval_kernel, sh, dim3((unsigned)g), lds, s, k);
   DPPO_LAUNCH_CHECK();
+  if (k.row > 0) {
+    DPPO_LAUNCH(next_eval_kernel, dim3((unsigned)g), dim3(kThreads), lds, s, k);
+    DPPO_LAUNCH_CHECK();
+  }
   return DPPO_OK;
 }
 
