@@ -416,20 +416,29 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
             __builtin_amdgcn_sched_barrier(0);
             fetch(k - 2, (k - 2) % 3);
           }
+          // The 16 dependent steps, in both arms of the re-read test: with one copy after the
+          // join, the join's wait had to cover the re-read arm's loads (s_waitcnt lgkmcnt(0)), so
+          // the fast arm also waited for chunk k-2's prefetch, issued just above -- one LDS round
+          // trip under the owners' traffic exposed in front of every chunk.
+          auto chain = [&]() {
+#ifndef DPPO_GAE_NOSCAN
+            f32x4 av[4];
+#pragma unroll
+            for (int j = kPChunk - 1; j >= 0; --j) {
+              a = gae_carry(d[b][j >> 2][j & 3], cf[b][j >> 2][j & 3], a);
+              av[j >> 2][j & 3] = a;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][k * kPChunk + 4 * q] = av[q];
+#endif
+          };
           if (pf[k] < gen) {  // prefetched before its owner published it: wait and re-read
             wait_flag(&L.loaded[k], gen);
             fetch(k, b);
+            chain();
+          } else {
+            chain();
           }
-#ifndef DPPO_GAE_NOSCAN
-          f32x4 av[4];
-#pragma unroll
-          for (int j = kPChunk - 1; j >= 0; --j) {
-            a = gae_carry(d[b][j >> 2][j & 3], cf[b][j >> 2][j & 3], a);
-            av[j >> 2][j & 3] = a;
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][k * kPChunk + 4 * q] = av[q];
-#endif
           if (lane == 0) set_flag(&L.scanned[k], gen);
           GAE_STAMP(33 + k);
         }

@@ -101,7 +101,7 @@ struct WLds {   // offsets in floats (compile-time: one layout per input width)
   int bo, bv, ls;  // [8], [4], [8]
   int gc;       // [4][8]: 1/(2 var), 1/var, 1/sigma, log sigma per action (continuous)
   int gent;     // [4]: {sum entropy terms, sum log-prob constants}
-  int W1, RS1;  // W1 [64][RS1]
+  int W1, RS1;  // W1 image [64 rows][RS1 >= D16], k-step-major per lane (layer1_w1)
   int total;
 };
 
@@ -355,6 +355,38 @@ __device__ __forceinline__ void bwdP(f32x4 (&t)[4], const float* W, const f32x4 
   SG_FENCE();
 }
 
+// bwdP of two matrices into the same tiles (t += W^T dz + U^T du) as ONE 32-k-step pipeline: the
+// second matrix's first rows are read during the first one's last k-steps instead of in a
+// pipeline restart whose first MFMAs wait for their reads.
+// The B operands of the first two k-steps (pre[0..1], bwdP_row(W, 0 / 1)) are read by the caller
+// one phase early, so that the pipeline's first MFMAs do not wait for them.
+__device__ __forceinline__ f32x4 bwdP_row(const float* W, int k, int q, int r) {
+  return *(const f32x4*)(W + (16 * (k >> 2) + (k & 3)) * kWS + ABL_BWD(q, r));
+}
+__device__ __forceinline__ void bwdP2(f32x4 (&t)[4], const float* W, const f32x4 (&dz)[4],
+                                      const float* U, const f32x4 (&du)[4], int q, int r,
+                                      const f32x4 (&pre)[2]) {
+  SG_FENCE();
+  f32x4 b[3];
+  auto ld = [&](int k) { return bwdP_row(k < 16 ? W : U, k & 15, q, r); };
+  b[0] = pre[0];
+  b[1] = pre[1];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if (k + 2 < 32) b[(k + 2) % 3] = ld(k + 2);
+    const int kk = k & 15;
+    const float av = k < 16 ? dz[kk >> 2][kk & 3] : du[kk >> 2][kk & 3];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) t[rb] = mfma4(av, b[k % 3][rb], t[rb]);
+  }
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    if (k + 2 < 32) SG_DSR(1);
+    SG_MFMA(4);
+  }
+  SG_FENCE();
+}
+
 // dW tiles += dZ X^T over the group's 16 samples (both operands in P layout, or X in the natural
 // T layout of the input features for dW1).
 template <int NIB>
@@ -423,6 +455,17 @@ struct GRec {
   f32x4 ca[2];        // continuous action of sample r (<= 8 dims)
   int sn;             // sample r's record (kLateCa: the action is read in the group's phase 3)
 };
+
+// Which instantiations hold the head rows in registers from the critic layer to the head
+// back-propagation: up to 4 heads (spill-free; with 6-8 heads ROCm 7.2's compiler crashes in
+// register allocation).  -DDPPO_MBW_PREHEADS=0 turns it off (A/B builds).
+#ifndef DPPO_MBW_PREHEADS
+#define DPPO_MBW_PREHEADS 1
+#endif
+template <int AMAX, bool CONT, int NIB>
+constexpr bool kPreloadHeads() {
+  return DPPO_MBW_PREHEADS && AMAX <= 4;
+}
 
 // X1: exactly 17 inputs (HalfCheetah).  Input column 16 is the only live one of the second
 // 16-column block, so its dW1 column is a VALU rank-1 sum (16 FMAs per group) instead of four
@@ -509,7 +552,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   // ---------------- prologue: weights into LDS -- every load is issued before the first store (a
   // load-store loop waits one memory round trip per iteration)
   constexpr int kWLd = 3 * (kMat / 4) / kThreadsW;           // 12 f32x4 of W2 | Wa | Wc per thread
-  constexpr int kW1Ld = (H * L.RS1 + kThreadsW - 1) / kThreadsW;
+  // W1 image: element k = ((row * 4 + q) * 4 NIB + t) holds W1[row][4t + q], so that lane (q, r)
+  // reads the A operands of all its layer-1 k-steps for output block ob as NIB ds_read_b128 at
+  // ((16 ob + r) * 4 + q) * 4 NIB (read one float at a time, every k-step's read was waited for
+  // right before its MFMA: 4-20 exposed LDS round trips per group)
+  constexpr int kW1N = H * 16 * NIB;
+  constexpr int kW1Ld = (kW1N + kThreadsW - 1) / kThreadsW;
+  static_assert(kW1N <= H * L.RS1, "W1 image");
   static_assert(3 * (kMat / 4) % kThreadsW == 0 && 4 * H == kThreadsW, "prologue split");
   f32x4 wld[kWLd];
   float w1ld[kW1Ld];
@@ -523,8 +572,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
   for (int i = 0; i < kW1Ld; ++i) {
     const int k = tid + i * kThreadsW;
-    const int row = k / L.RS1, c = k - row * L.RS1;
-    const bool on = k < H * L.RS1 && c < D;
+    const int t = k % (4 * NIB), qq = (k / (4 * NIB)) & 3, row = k / (16 * NIB), c = 4 * t + qq;
+    const bool on = k < kW1N && c < D;
     w1ld[i] = P[po.W1 + (on ? row * D + c : 0)];
   }
   const float wold = P[po.Wo + ((tid >> 6) < a.A ? tid : 0)];
@@ -540,8 +589,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
   for (int i = 0; i < kW1Ld; ++i) {
     const int k = tid + i * kThreadsW;
-    const int row = k / L.RS1, c = k - row * L.RS1;
-    if (k < H * L.RS1) lds[L.W1 + k] = c < D ? w1ld[i] * kTS : 0.0f;
+    const int t = k % (4 * NIB), c = 4 * t + ((k / (4 * NIB)) & 3);
+    if (k < kW1N) lds[L.W1 + k] = c < D ? w1ld[i] * kTS : 0.0f;
   }
   lds[L.Wo + tid] = (tid >> 6) < a.A ? wold : 0.0f;
   lds[L.Wo + 4 * H + tid] = (tid >> 6) + 4 < a.A ? wold2 : 0.0f;
@@ -616,12 +665,17 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   auto layer1 = [&](f32x4 (&h)[4], const GRec<NIB>& g) {
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) h[ob] = *(const f32x4*)(lds + L.b1 + 16 * ob + 4 * q);
+    f32x4 w1[4][NIB];
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int tb = 0; tb < NIB; ++tb)
+        w1[ob][tb] = *(const f32x4*)(lds + L.W1 + ((16 * ob + r) * 4 + q) * 4 * NIB + 4 * tb);
 #pragma unroll
     for (int t = 0; t < 4 * NIB; ++t) {
       if (t < a.nkn) {
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-          h[ob] = mfma4(lds[L.W1 + (16 * ob + r) * L.RS1 + 4 * t + q], g.xn[t], h[ob]);
+        for (int ob = 0; ob < 4; ++ob) h[ob] = mfma4(w1[ob][t >> 2][t & 3], g.xn[t], h[ob]);
       }
     }
     tanh4(h);
@@ -666,6 +720,28 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       g_cur.ca[0] = *(const f32x4*)(rn + 4);
       g_cur.ca[1] = *(const f32x4*)(rn + 8);
     }
+    // the head rows this lane dots (actor heads and the value head), read before the critic
+    // layer's MFMAs: read at their use, every row cost one exposed LDS round trip (the scheduler
+    // placed each read right before its dot product, after the last MFMA)
+    constexpr bool kPreHeads = kPreloadHeads<AMAX, CONT, NIB>();
+    // 5-8 heads: the heads are one MFMA output tile instead (A = head row r & 7, the lane's
+    // features 16 kb + 4q .. + 3 as for a hidden layer; B = a1): 16 MFMAs against AMAX x 16 VALU
+    // FMAs + 4 LDS round trips per head
+    constexpr bool kMfmaHeads = AMAX > 4;
+    f32x4 wo[kPreHeads ? AMAX : 1][4], wv[4], woT[4];
+    if (kMfmaHeads) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) woT[kb] = *(const f32x4*)(lds + L.Wo + (r & 7) * H + 16 * kb + 4 * q);
+    }
+    if (kPreHeads) {
+#pragma unroll
+      for (int h = 0; h < AMAX; ++h)
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob)
+          wo[h][ob] = *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob) wv[ob] = *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q);
+    }
     SG_FENCE();
     {
       fwd64_raw(c1, Wc, h2, q, r);
@@ -673,11 +749,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       put_n(sx, a1, q, r);
       // ---- (4) heads: logits / means and value of sample r, in every lane of the sample
 #pragma unroll
-      for (int h = 0; h < AMAX; ++h) {
+      for (int h = 0; h < (kMfmaHeads ? 0 : AMAX); ++h) {
         float s = 0.f;
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob)
-          s += dot4(*(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q), a1[ob]);
+          s += dot4(kPreHeads ? wo[kPreHeads ? h : 0][ob]
+                              : *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q),
+                    a1[ob]);
         out[h] = qsum(s) + lds[L.bo + h];
       }
       SG_DSR(4 + 4 * AMAX);
@@ -694,6 +772,31 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         }
       SG_FENCE();
     }
+    if (kMfmaHeads) {
+      // two accumulation chains (even / odd k-steps), then tile register v of lane (q, r) = head
+      // 4q + v of sample r: rows q = 0 / 1 carry heads 0-3 / 4-7; permlane16_swap gives rows 0-1
+      // {row 0, row 1}, permlane32_swap broadcasts the lower half to all four rows
+      f32x4 ha = z4(), hb = z4();
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        ha = mfma4(woT[kb][0], a1[kb][0], ha);
+        hb = mfma4(woT[kb][1], a1[kb][1], hb);
+        ha = mfma4(woT[kb][2], a1[kb][2], ha);
+        hb = mfma4(woT[kb][3], a1[kb][3], hb);
+      }
+      const f32x4 ht = ha + hb;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(ht[v]),
+                                                        __float_as_uint(ht[v]), false, false);
+        const auto lo = __builtin_amdgcn_permlane32_swap(p[0], p[0], false, false);
+        out[v] = __uint_as_float(lo[0]) + lds[L.bo + v];
+        if (4 + v < AMAX) {
+          const auto hi = __builtin_amdgcn_permlane32_swap(p[1], p[1], false, false);
+          out[4 + v] = __uint_as_float(hi[0]) + lds[L.bo + 4 + v];
+        }
+      }
+    }
     tanh4(c1);
     put_n(sy, c1, q, r);
     PHASE_FENCE();
@@ -701,7 +804,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     float vpart = 0.f;
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
-      vpart += dot4(*(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q), c1[ob]);
+      vpart += dot4(kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q), c1[ob]);
     const float val = qsum(vpart) + lds[L.bv];
     // ---- (5) per-sample loss and head deltas (ppo.py:264-280)
     const f32x4 sc = g_cur.sc;
@@ -781,6 +884,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     WSTAMP(k, 4);
     // ---- (6) head weight gradients (P layout: feature 4r + cb, samples 4q + v), then the head
     // back-propagation dza = (Wo^T dl)(1 - a1^2), dzc = Wv dv (1 - c1^2) in the N layout
+    // (not in the 4-discrete-action instantiation: it would spill 6 registers there)
+    constexpr bool kPreDh2 = !(AMAX == 4 && !CONT && NIB == 1);
+    f32x4 dh2_pre[2];
+    if (kPreDh2) {
+      dh2_pre[0] = bwdP_row(Wa, 0, q, r);
+      dh2_pre[1] = bwdP_row(Wa, 1, q, r);
+    }
     {
       f32x4 a1t[4], c1t[4];
       get_p(a1t, sx, q, r);
@@ -811,14 +921,28 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       }
     }
     f32x4 dza[4], dzc[4];
+    // 5-8 heads: Wo^T dl on MFMA (k = head, two k-steps; A = Wo[4ks + q][16 ob + r], B = the
+    // delta of head 4ks + q of sample r), the N layout directly
+    float bsel[2];
+#pragma unroll
+    for (int ks = 0; ks < (kMfmaHeads ? 2 : 0); ++ks)
+      bsel[ks] = q == 0 ? dl[4 * ks] : (q == 1 ? dl[4 * ks + 1] : (q == 2 ? dl[4 * ks + 2] : dl[4 * ks + 3]));
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) {
       f32x4 da = z4();
+      if (kMfmaHeads) {
 #pragma unroll
-      for (int h = 0; h < AMAX; ++h)
-        da += *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q) * dl[h];
+        for (int ks = 0; ks < 2; ++ks)
+          da = mfma4(lds[L.Wo + (4 * ks + q) * H + 16 * ob + r], bsel[ks], da);
+      } else {
+#pragma unroll
+        for (int h = 0; h < AMAX; ++h)
+          da += (kPreHeads ? wo[kPreHeads ? h : 0][ob]
+                           : *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q)) * dl[h];
+      }
       dza[ob] = da * (1.0f - a1[ob] * a1[ob]);
-      dzc[ob] = (*(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q) * dv) * (1.0f - c1[ob] * c1[ob]);
+      dzc[ob] = ((kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q)) * dv) *
+                (1.0f - c1[ob] * c1[ob]);
     }
     put_n(sx, dza, q, r);
     put_n(sy, dzc, q, r);
@@ -841,8 +965,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         }
     }
     f32x4 dh2[4] = {z4(), z4(), z4(), z4()};
-    bwdP(dh2, Wa, dza, q, r);
-    bwdP(dh2, Wc, dzc, q, r);
+    if (!kPreDh2) {
+      dh2_pre[0] = bwdP_row(Wa, 0, q, r);
+      dh2_pre[1] = bwdP_row(Wa, 1, q, r);
+    }
+    bwdP2(dh2, Wa, dza, Wc, dzc, q, r, dh2_pre);
     // the next group's records (its indices came one group ago) and the indices after that
     GRec<NIB> g_nxt{};
     if (k + 1 < nk) g_nxt = gather(f_nxt);
