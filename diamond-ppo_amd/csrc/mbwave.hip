@@ -254,11 +254,16 @@ __device__ __forceinline__ float dot4(f32x4 w, f32x4 x) {
 
 // Forward of one hidden layer, N -> N: y[ob] += W[16ob + i][:] x for the four 16-row output
 // blocks; the A operand of k-steps (kb, 0..3) is one ds_read_b128 of the row.
-__device__ __forceinline__ void fwd64_raw(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4],
-                                          int q, int r) {
+// The A operands of k-block 0 (fwd64_first), read by the caller ahead of the layer or here.
+__device__ __forceinline__ void fwd64_first(f32x4 (&w0)[4], const float* W, int q, int r) {
+#pragma unroll
+  for (int ob = 0; ob < 4; ++ob) w0[ob] = *(const f32x4*)(W + 16 * ob * kWS + ABL_FWD(q, r));
+}
+__device__ __forceinline__ void fwd64_pre(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4],
+                                          int q, int r, const f32x4 (&w0)[4]) {
   f32x4 w[2][4];
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob) w[0][ob] = *(const f32x4*)(W + 16 * ob * kWS + ABL_FWD(q, r));
+  for (int ob = 0; ob < 4; ++ob) w[0][ob] = w0[ob];
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
     if (kb + 1 < 4) {
@@ -271,6 +276,12 @@ __device__ __forceinline__ void fwd64_raw(f32x4 (&y)[4], const float* W, const f
 #pragma unroll
       for (int ob = 0; ob < 4; ++ob) y[ob] = mfma4(w[kb & 1][ob][v], x[kb][v], y[ob]);
   }
+}
+__device__ __forceinline__ void fwd64_raw(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4],
+                                          int q, int r) {
+  f32x4 w0[4];
+  fwd64_first(w0, W, q, r);
+  fwd64_pre(y, W, x, q, r, w0);
 }
 __device__ __forceinline__ void fwd64(f32x4 (&y)[4], const float* W, const f32x4 (&x)[4], int q,
                                       int r) {
@@ -578,6 +589,29 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   }
   const float wold = P[po.Wo + ((tid >> 6) < a.A ? tid : 0)];
   const float wold2 = P[po.Wo + ((tid >> 6) + 4 < a.A ? tid + 4 * H : 0)];
+  // the small parameters with the weights (loaded where they are stored, behind the weight
+  // stores, they cost one more memory round trip before the barrier): Wv, b1, b2, ba, bc of
+  // feature tid (tid < H); bo, log std of head h = tid - H and bv (H <= tid < H + 8); every log
+  // std for the entropy sums (continuous)
+  // (not in the 4-discrete-action instantiation, which has no registers to spare: its main loop
+  // would spill)
+  constexpr bool kTight = AMAX == 4 && !CONT && NIB == 1;
+  const int fs = tid < H ? tid : 0;
+  const int hs = (tid >= H && tid - H < a.A) ? tid - H : 0;
+  float sWv = 0.f, sb1 = 0.f, sb2 = 0.f, sba = 0.f, sbc = 0.f, sbo = 0.f, sls = 0.f, sbv = 0.f;
+  float lsv[8];
+  if (!kTight) {
+    sWv = P[po.Wv + fs];
+    sb1 = P[po.b1 + fs];
+    sb2 = P[po.b2 + fs];
+    sba = P[po.ba + fs];
+    sbc = P[po.bc + fs];
+    sbo = P[po.bo + hs];
+    sls = CONT ? P[po.ls + hs] : 0.0f;
+    sbv = P[po.bv];
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) lsv[k] = CONT ? P[po.ls + (k < a.A ? k : 0)] : 0.0f;
   GRec<NIB> g_cur{};
   if (nk > 0) g_cur = gather(f_cur);
 #pragma unroll
@@ -595,31 +629,36 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   lds[L.Wo + tid] = (tid >> 6) < a.A ? wold : 0.0f;
   lds[L.Wo + 4 * H + tid] = (tid >> 6) + 4 < a.A ? wold2 : 0.0f;
   if (tid < H) {
-    lds[L.Wv + tid] = P[po.Wv + tid];
-    lds[L.b1 + tid] = P[po.b1 + tid] * kTS;
-    lds[L.b2 + tid] = P[po.b2 + tid] * kTS;
-    lds[L.ba + tid] = P[po.ba + tid] * kTS;
-    lds[L.bc + tid] = P[po.bc + tid] * kTS;
+    lds[L.Wv + tid] = kTight ? P[po.Wv + tid] : sWv;
+    lds[L.b1 + tid] = (kTight ? P[po.b1 + tid] : sb1) * kTS;
+    lds[L.b2 + tid] = (kTight ? P[po.b2 + tid] : sb2) * kTS;
+    lds[L.ba + tid] = (kTight ? P[po.ba + tid] : sba) * kTS;
+    lds[L.bc + tid] = (kTight ? P[po.bc + tid] : sbc) * kTS;
   } else if (tid < H + 8) {
     const int h = tid - H;
-    lds[L.bo + h] = h < a.A ? P[po.bo + h] : 0.0f;
-    lds[L.ls + h] = (CONT && h < a.A) ? P[po.ls + h] : 0.0f;
-    if (h < 4) lds[L.bv + h] = h == 0 ? P[po.bv] : 0.0f;
+    lds[L.bo + h] = h < a.A ? (kTight ? P[po.bo + h] : sbo) : 0.0f;
+    lds[L.ls + h] = (CONT && h < a.A) ? (kTight ? P[po.ls + h] : sls) : 0.0f;
+    if (h < 4) lds[L.bv + h] = h == 0 ? (kTight ? P[po.bv] : sbv) : 0.0f;
     if (CONT) {
       // Normal(mean, exp(log_std)) constants of action h (continuous_ppo.py:41-47; torch
       // Normal.log_prob / entropy), the same for every sample
       const bool on = h < a.A;
-      const float sg = on ? __expf(P[po.ls + h]) : 1.0f;
+      const float sg = on ? __expf(kTight ? P[po.ls + h] : sls) : 1.0f;
       lds[L.gc + h] = on ? 1.0f / (2.0f * (sg * sg)) : 0.0f;
       lds[L.gc + 8 + h] = 1.0f / (sg * sg);
       lds[L.gc + 16 + h] = 1.0f / sg;
       lds[L.gc + 24 + h] = on ? __logf(sg) : 0.0f;
       if (h == 0) {
+        // (the log-std values were loaded above: a run-time bounded loop here issued the loads
+        // one round trip at a time)
         float e = 0.0f, c = 0.0f;
-        for (int k = 0; k < a.A && k < 8; ++k) {
-          const float l = __logf(__expf(P[po.ls + k]));
-          e += kHalfLog2PiPlusHalfW + l;  // entropy (continuous_ppo.py:45-47)
-          c += l + kLogSqrt2PiW;           // log-prob constant part
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (k < a.A) {
+            const float l = __logf(__expf(lsv[k]));
+            e += kHalfLog2PiPlusHalfW + l;  // entropy (continuous_ppo.py:45-47)
+            c += l + kLogSqrt2PiW;           // log-prob constant part
+          }
         }
         lds[L.gent] = e;
         lds[L.gent + 1] = c;
@@ -884,8 +923,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     WSTAMP(k, 4);
     // ---- (6) head weight gradients (P layout: feature 4r + cb, samples 4q + v), then the head
     // back-propagation dza = (Wo^T dl)(1 - a1^2), dzc = Wv dv (1 - c1^2) in the N layout
-    // (not in the 4-discrete-action instantiation: it would spill 6 registers there)
-    constexpr bool kPreDh2 = !(AMAX == 4 && !CONT && NIB == 1);
+    constexpr bool kPreDh2 = !kTight;  // (it would spill 6 registers there)
     f32x4 dh2_pre[2];
     if (kPreDh2) {
       dh2_pre[0] = bwdP_row(Wa, 0, q, r);
@@ -979,9 +1017,10 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     // ---- (8) dz2 = dh2 (1 - h2^2); hidden-bias partials; dWa, dWc
     {
       f32x4 h2t[4], dzat[4], dzct[4], dz2t[4];
+      // h2t first: dz2t needs only it, so its VALU runs while dzat / dzct land
+      get_p(h2t, sh2, q, r);
       get_p(dzat, sx, q, r);
       get_p(dzct, sy, q, r);
-      get_p(h2t, sh2, q, r);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         dz2t[b] = dh2[b] * (1.0f - h2t[b] * h2t[b]);

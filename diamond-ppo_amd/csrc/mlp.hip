@@ -232,14 +232,23 @@ __device__ __forceinline__ void heads(float (&out)[AMAX], const float* Wo, const
   for (int a = 0; a < AMAX; ++a) {
     float part = 0.0f;
     if (a < A) {
+      // the row's eight 16-B slices read together (one at a time, each read was waited for
+      // right before its dot product)
+      // (16 heads: their instantiation would spill, one read at a time there)
       const float* wp = Wo + a * H + 4 * h;
+      f32x4 w[2][4];
+#pragma unroll
+      for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (AMAX <= 8) w[fb][q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
 #pragma unroll
       for (int fb = 0; fb < 2; ++fb)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x4 w = *(const f32x4*)(wp + fb * 32 + 8 * q);
-          part += w[0] * x[fb][4 * q + 0] + w[1] * x[fb][4 * q + 1] + w[2] * x[fb][4 * q + 2] +
-                  w[3] * x[fb][4 * q + 3];
+          const f32x4 wq = AMAX <= 8 ? w[fb][q] : *(const f32x4*)(wp + fb * 32 + 8 * q);
+          part += wq[0] * x[fb][4 * q + 0] + wq[1] * x[fb][4 * q + 1] +
+                  wq[2] * x[fb][4 * q + 2] + wq[3] * x[fb][4 * q + 3];
         }
     }
     out[a] = half_sum(part) + bo[a];
@@ -250,14 +259,17 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
                                             int h) {
   float part = 0.0f;
   const float* wp = Wv + 4 * h;
+  f32x4 w[2][4];  // read together (heads above)
 #pragma unroll
   for (int fb = 0; fb < 2; ++fb)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w = *(const f32x4*)(wp + fb * 32 + 8 * q);
-      part += w[0] * x[fb][4 * q + 0] + w[1] * x[fb][4 * q + 1] + w[2] * x[fb][4 * q + 2] +
-              w[3] * x[fb][4 * q + 3];
-    }
+    for (int q = 0; q < 4; ++q) w[fb][q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
+#pragma unroll
+  for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      part += w[fb][q][0] * x[fb][4 * q + 0] + w[fb][q][1] * x[fb][4 * q + 1] +
+              w[fb][q][2] * x[fb][4 * q + 2] + w[fb][q][3] * x[fb][4 * q + 3];
   return half_sum(part) + bv;
 }
 

@@ -28,7 +28,8 @@ CLASS = {"mb_kernel": "grad", "mbw_kernel": "grad", "grad_kernel": "grad", "eval
          "clip_adam_kernel": "clip_adam", "reduce_adam_kernel": "reduce_adam",
          "stats_reduce_kernel": "adv_stats", "fy_build_kernel": "perm",
          "fy_links_kernel": "perm", "fy_solve_kernel": "perm", "shard_count_kernel": "perm",
-         "shard_write_kernel": "perm"}
+         "shard_write_kernel": "perm", "next_eval_kernel": "next_eval",
+         "gae_aff_kernel": "gae"}
 
 
 def short(name: str) -> str:
