@@ -34,6 +34,8 @@ constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 // MFMAs then produce kTS z and tanh_inplace skips its multiply (one VALU instruction fewer per
 // activation; VALU is not hidden behind fp32 MFMAs on gfx950).
 constexpr float kTS = 2.8853900817779268f;
+constexpr int kQueueCap = 256;  // queued samples a wave holds before it flushes them (>= 32)
+constexpr int kMatchRound = 4;  // next_obs / obs feature pairs compared per round of loads
 
 struct LdsLayout {
   int W1, S1;          // W1 image [H][S1], S1 = D8 + 4 (zero-padded columns D..S1)
@@ -44,6 +46,7 @@ struct LdsLayout {
   int bo, ls;          // [32]
   int bv;              // [4]
   int weights_end;
+  int queue;           // [kWaves][kQueueCap] int32 (eval_kernel, next-value reuse)
   int total;           // floats
 };
 
@@ -86,6 +89,7 @@ LdsLayout make_layout(const MlpShape& sh) {
   L.ls = o; o += 32;
   L.bv = o; o += 4;
   L.weights_end = o;
+  L.queue = o; o += kWaves * kQueueCap;  // eval_kernel (reuse mode): per-wave sample queues
   L.total = o;
   return L;
 }
@@ -232,24 +236,23 @@ __device__ __forceinline__ void heads(float (&out)[AMAX], const float* Wo, const
   for (int a = 0; a < AMAX; ++a) {
     float part = 0.0f;
     if (a < A) {
-      // the row's eight 16-B slices read together (one at a time, each read was waited for
-      // right before its dot product)
+      // a 32-feature block's four 16-B slices read together (one at a time, each read was
+      // waited for right before its dot product)
       // (16 heads: their instantiation would spill, one read at a time there)
       const float* wp = Wo + a * H + 4 * h;
-      f32x4 w[2][4];
 #pragma unroll
-      for (int fb = 0; fb < 2; ++fb)
+      for (int fb = 0; fb < 2; ++fb) {
+        f32x4 w[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (AMAX <= 8) w[fb][q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
-#pragma unroll
-      for (int fb = 0; fb < 2; ++fb)
+          if (AMAX <= 8) w[q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x4 wq = AMAX <= 8 ? w[fb][q] : *(const f32x4*)(wp + fb * 32 + 8 * q);
+          const f32x4 wq = AMAX <= 8 ? w[q] : *(const f32x4*)(wp + fb * 32 + 8 * q);
           part += wq[0] * x[fb][4 * q + 0] + wq[1] * x[fb][4 * q + 1] +
                   wq[2] * x[fb][4 * q + 2] + wq[3] * x[fb][4 * q + 3];
         }
+      }
     }
     out[a] = half_sum(part) + bo[a];
   }
@@ -259,17 +262,16 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
                                             int h) {
   float part = 0.0f;
   const float* wp = Wv + 4 * h;
-  f32x4 w[2][4];  // read together (heads above)
 #pragma unroll
-  for (int fb = 0; fb < 2; ++fb)
+  for (int fb = 0; fb < 2; ++fb) {
+    f32x4 w[4];  // a block's four slices read together (heads above)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) w[fb][q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
-#pragma unroll
-  for (int fb = 0; fb < 2; ++fb)
+    for (int q = 0; q < 4; ++q) w[q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      part += w[fb][q][0] * x[fb][4 * q + 0] + w[fb][q][1] * x[fb][4 * q + 1] +
-              w[fb][q][2] * x[fb][4 * q + 2] + w[fb][q][3] * x[fb][4 * q + 3];
+      part += w[q][0] * x[fb][4 * q + 0] + w[q][1] * x[fb][4 * q + 1] +
+              w[q][2] * x[fb][4 * q + 2] + w[q][3] * x[fb][4 * q + 3];
+  }
   return half_sum(part) + bv;
 }
 
@@ -306,12 +308,30 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
   const LdsLayout& L = a.L;
   const float bv = lds_[L.bv];
   const int64_t ntiles = (a.n + 31) / 32;
+  // Reuse mode: the samples whose next value needs the critic pass are queued in a wave-private
+  // LDS list and appended to the global list a queue at a time -- one returning atomic per flush
+  // instead of one per tile, each of which held the wave for a device-scope round trip.
+  // (queue offset and fill count kept wave-uniform -- scalar registers: the vector ones are all
+  // taken at four waves per SIMD)
+  const int qbase = L.queue + __builtin_amdgcn_readfirstlane(wave) * kQueueCap;
+  int qn = 0;
+  auto flush = [&]() {
+    if (qn == 0) return;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(a.list_ctr + a.par, (unsigned)qn);
+    base = __shfl(base, 0);
+    for (int k = lane; k < qn; k += kWave) a.list[base + k] = ((const int32_t*)lds_)[qbase + k];
+    qn = 0;
+  };
   for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles;
        tile += (int64_t)gridDim.x * kWaves) {
     float* lds = opaque_base(lds_);
     const int64_t i = tile * 32 + l31;
     const bool valid = i < a.n;
     const int64_t ic = valid ? i : 0;
+    // the sampled action (categorical), requested with the observation: read at its use after
+    // the heads, it was one more memory round trip per tile
+    const int act_d = CONT ? 0 : ((const int32_t*)a.actions)[ic];
     // ---- obs: full actor-critic forward (get_logits_and_values, ppo.py:91-96)
     f32x16 x[2], y[2];
     x[0] = load_x0_obs(a.obs + ic * a.D, a.D, a.nq1, valid, h);
@@ -338,7 +358,7 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       }
     } else {
       // Categorical(logits).log_prob (torch distributions/categorical.py:78,156)
-      const int act = ((const int32_t*)a.actions)[ic];
+      const int act = act_d;
       float mx = out[0];
 #pragma unroll
       for (int k = 1; k < AMAX; ++k)
@@ -361,20 +381,31 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       if (valid && h == 0) {
         bool m = i + a.row < a.n;
         if (m) {
+          // kMatchRound features per round, all their loads in flight together (a short-circuit
+          // loop waited for every pair: D memory round trips per tile)
           const uint32_t* p = (const uint32_t*)(a.next_obs + ic * a.D);
           const uint32_t* o = (const uint32_t*)(a.obs + (ic + a.row) * a.D);
-          for (int f = 0; f < a.D; ++f) m = m && p[f] == o[f];
+          for (int f0 = 0; f0 < a.D; f0 += kMatchRound) {
+            uint32_t pv[kMatchRound], ov[kMatchRound];
+#pragma unroll
+            for (int j = 0; j < kMatchRound; ++j) {
+              const int f = f0 + j < a.D ? f0 + j : a.D - 1;
+              pv[j] = p[f];
+              ov[j] = o[f];
+            }
+#pragma unroll
+            for (int j = 0; j < kMatchRound; ++j) m = m & (pv[j] == ov[j]);
+          }
         }
         a.match[i] = m ? 1 : 0;
         need = !m;
       }
       const uint64_t bal = __ballot(need);
       if (bal != 0) {
-        const int first = __builtin_ctzll(bal);
-        unsigned base = 0;
-        if (lane == first) base = atomicAdd(a.list_ctr + a.par, (unsigned)__popcll(bal));
-        base = __shfl(base, first);
-        if (need) a.list[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)i;
+        const int cnt = __builtin_amdgcn_readfirstlane(__popcll(bal));
+        if (qn + cnt > kQueueCap) flush();
+        if (need) ((int32_t*)lds_)[qbase + qn + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)i;
+        qn = __builtin_amdgcn_readfirstlane(qn + cnt);
       }
       if (valid && h == 0) {
         a.logp[i] = logp;
@@ -394,6 +425,7 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       a.next_values[i] = nv;
     }
   }
+  flush();
 }
 
 // The critic pass on next_obs for the samples eval_kernel queued (reuse mode), and the reused
@@ -404,14 +436,22 @@ __global__ __launch_bounds__(kThreads, 4) void next_eval_kernel(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds_[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l31 = lane & 31, h = lane >> 5;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + tid; i < a.n;
-       i += (int64_t)gridDim.x * kThreads)
-    if (a.match[i]) a.next_values[i] = a.values[i + a.row];
+  // the reused values (a streaming copy) after this workgroup's critic tiles (a latency-bound
+  // chain of dependent layers): the workgroups without a tile copy at once, the others overlap
+  // their tiles with them
+  auto copy_reused = [&]() {
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + tid; i < a.n;
+         i += (int64_t)gridDim.x * kThreads)
+      if (a.match[i]) a.next_values[i] = a.values[i + a.row];
+  };
   const unsigned cnt = __hip_atomic_load(a.list_ctr + a.par, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x == 0 && tid == 0) a.list_ctr[a.par ^ 1] = 0u;
   const int64_t ntiles = ((int64_t)cnt + 31) / 32;
-  if ((int64_t)blockIdx.x * kWaves >= ntiles) return;  // no tile for this workgroup
+  if ((int64_t)blockIdx.x * kWaves >= ntiles) {  // no tile for this workgroup
+    copy_reused();
+    return;
+  }
   load_weights(lds_, a, tid);
   __syncthreads();
   const LdsLayout& L = a.L;
@@ -430,6 +470,7 @@ __global__ __launch_bounds__(kThreads, 4) void next_eval_kernel(KArgs a) {
     const float nv = value_head(lds + L.Wv, bv, y, h);
     if (valid && h == 0) a.next_values[i] = nv;
   }
+  copy_reused();
 }
 
 // ------------------------------------------------------------------------------------------------
