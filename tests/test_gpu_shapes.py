@@ -43,8 +43,26 @@ def _shapes():
     return out
 
 
+# One shape per head path of the sample-split kernel (mbwave.hip, round 3): head rows held in
+# registers (<= 4 heads: 1-2 and 3-4 action rows, one or two input blocks), the heads and their
+# back-propagation as MFMA tiles (5-8 categorical actions; 5-6 Gaussian actions on 17 inputs,
+# HalfCheetah's X1 layout), each with a partial last 16-sample group.
+_HEAD_SHAPES = [(4, 2, False), (3, 1, True), (8, 3, False), (8, 4, False), (11, 4, True),
+                (20, 3, False), (16, 5, False), (8, 7, False), (16, 8, False), (17, 5, True),
+                (17, 6, True)]
+
+
+@pytest.mark.parametrize("j,D,A,cont", [(j, *s) for j, s in enumerate(_HEAD_SHAPES)])
+def test_minibatch_gradient_head_paths(j, D, A, cont):
+    _check(100 + j, D, A, cont, 16, 96, 4, 5)
+
+
 @pytest.mark.parametrize("i,D,A,cont,T,Nn,M,ragged", _shapes())
 def test_minibatch_gradient_shape_sweep(i, D, A, cont, T, Nn, M, ragged):
+    _check(i, D, A, cont, T, Nn, M, ragged)
+
+
+def _check(i, D, A, cont, T, Nn, M, ragged):
     B = T * Nn
     h = N.Handle(0, N.Dims(T, Nn, D, A, int(cont), H, 4, M, 1, 0))
     L = h.layout
