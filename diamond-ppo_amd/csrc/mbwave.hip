@@ -840,6 +840,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     put_n(sy, c1, q, r);
     PHASE_FENCE();
     WSTAMP(k, 3);
+    // the actor / critic hidden layers in the P layout for the head weight gradients of phase 6,
+    // requested now: they land during the loss chain instead of starting phase 6 with a wait
+    f32x4 a1t[4], c1t[4];
+    get_p(a1t, sx, q, r);
+    get_p(c1t, sy, q, r);
     float vpart = 0.f;
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
@@ -930,9 +935,6 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       dh2_pre[1] = bwdP_row(Wa, 1, q, r);
     }
     {
-      f32x4 a1t[4], c1t[4];
-      get_p(a1t, sx, q, r);
-      get_p(c1t, sy, q, r);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         if (kMfmaWo) {
@@ -1038,11 +1040,19 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     {
       f32x4 dz2[4], dz2t[4], h1t[4];
       get_n(dz2, sx, q, r);
+      // dz2 again in the P layout (from the same slot) and h1 for dW2, requested before the dh1
+      // MFMAs so that they land during them (after them in the 4-discrete-action instantiation,
+      // which would spill 2 registers)
+      if (!kTight) {
+        get_p(dz2t, sx, q, r);
+        get_p(h1t, sh1, q, r);
+      }
       f32x4 dh1[4] = {z4(), z4(), z4(), z4()};
       bwdP(dh1, W2, dz2, q, r);
-      // dz2 again in the P layout (from the same slot) and h1 for dW2
-      get_p(dz2t, sx, q, r);
-      get_p(h1t, sh1, q, r);
+      if (kTight) {
+        get_p(dz2t, sx, q, r);
+        get_p(h1t, sh1, q, r);
+      }
       // the next group's layer 1 (sh1 is free once h1t is read: one wave's LDS ops run in order)
       if (kHoistL1 && k + 1 < nk) layer1(h1, g_nxt);
       wgrad<4>(gW2, dz2t, h1t);
