@@ -221,6 +221,44 @@ __device__ __forceinline__ float gae_carry(float delta, float coef, float a) {
   return delta + coef * a;                    // ppo.py:213-219
 }
 
+// The normalisation statistics (ppo.py:243) of a row's 4 advantages, in fp32 and in a fixed
+// order; the caller adds one fp32 partial per chunk (<= 8 values) into its fp64 sums.  Per-value
+// fp64 accumulation cost 3 half-rate fp64 operations per value on the SIMD the scan runs on.
+__device__ __forceinline__ void stats4(const f32x4& av, float& s, float& q) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s += av[j];
+    q = __builtin_fmaf(av[j], av[j], q);
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ __forceinline__ double lane_f64(double x, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// Wave sum in a fixed order, the result valid in every lane: DPP within each 16-lane row (xor 1,
+// xor 2, half-row mirror, row mirror: VALU data moves, no LDS round trip), then the 4 row sums
+// read from lanes 0/16/32/48.  Replaces a 6-round ds_bpermute butterfly that sat at the end of
+// the launch, after the last stores.
+__device__ __forceinline__ double wave_sum_f64(double x) {
+  x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f64<0x141>(x);  // row_half_mirror
+  x += dpp_f64<0x140>(x);  // row_mirror
+  return (lane_f64(x, 0) + lane_f64(x, 16)) + (lane_f64(x, 32) + lane_f64(x, 48));
+}
+
 __device__ __forceinline__ void wait_flag(int* f, int gen) {
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
     __builtin_amdgcn_s_sleep(1);
@@ -336,14 +374,24 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
         GAE_STAMP(1 + k);
         wait_flag(&L.scanned[k], gen);
         GAE_STAMP(9 + k);
+        float s32 = 0.0f, q32 = 0.0f;
+        // every pass's advantages read before the first store: the write-through stores are asm
+        // with a memory clobber, so reads placed after one wait for their own LDS round trip
+        f32x4 avp[PER];
+#pragma unroll
+        for (int p = 0; p < PER; ++p) {
+          const int row = p * RP + lane / V4;
+          if (row < nr) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) avp[p][j] = L.a[e0 + j][r0 + row];
+          }
+        }
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
           const int row = p * RP + lane / V4;
           if (row < nr) {
             const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
-            f32x4 av;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
+            const f32x4 av = avp[p];
             if (wt) {
               store_wt(adv + go, av);
               store_wt(ret + go, xv[p] + av);  // returns = values + advantages (ppo.py:241)
@@ -351,22 +399,17 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
               *(f32x4*)(adv + go) = av;
               *(f32x4*)(ret + go) = xv[p] + av;
             }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              lsum += (double)av[j];
-              lsq += (double)av[j] * (double)av[j];
-            }
+            stats4(av, s32, q32);
           }
         }
+        lsum += (double)s32;
+        lsq += (double)q32;
         GAE_STAMP(17 + k);
       }
     }
-    // this wave's statistics partial (fixed shuffle tree)
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      lsum += __shfl_xor(lsum, off);
-      lsq += __shfl_xor(lsq, off);
-    }
+    // this wave's statistics partial (fixed order)
+    lsum = wave_sum_f64(lsum);
+    lsq = wave_sum_f64(lsq);
     if (lane == 0) {
       L.wsum[k][0] = lsum;
       L.wsum[k][1] = lsq;
@@ -397,9 +440,25 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
             cf[set][q] = *(const f32x4*)&L.coef[e][k * kPChunk + 4 * q];
           }
         };
-        wait_flag(&L.loaded[kPChunks - 1], gen);
+        // Wait for chunk k by polling its flag and its data together: the flag read is performed
+        // before the data reads (one wave's LDS operations complete in order), so the poll that
+        // sees the flag set already holds current data -- one LDS round trip after the owner's
+        // flag store instead of two (poll the flag, then fetch).
+        auto poll = [&](int k, int set) {
+          int f;
+          do {
+            f = __hip_atomic_load(&L.loaded[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_sched_barrier(0);
+            fetch(k, set);
+            // keep every poll's data reads in the loop (without a use, the compiler sinks them
+            // behind it: flag round trip, then data round trip)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(d[set][q]), "+v"(cf[set][q]));
+          } while (f < gen);
+        };
+        poll(kPChunks - 1, (kPChunks - 1) % 3);
         pf[kPChunks - 1] = gen;
-        fetch(kPChunks - 1, (kPChunks - 1) % 3);
         // speculative prefetch of chunk k-1 / k-2: its flag is read before its data (LDS
         // operations of one wave complete in order), so a set flag proves the data current
         pf[kPChunks - 2] =
@@ -432,9 +491,8 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
             for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][k * kPChunk + 4 * q] = av[q];
 #endif
           };
-          if (pf[k] < gen) {  // prefetched before its owner published it: wait and re-read
-            wait_flag(&L.loaded[k], gen);
-            fetch(k, b);
+          if (pf[k] < gen) {  // prefetched before its owner published it: poll and re-read
+            poll(k, b);
             chain();
           } else {
             chain();
@@ -598,6 +656,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
       if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
     }
     GAE_STAMP(33 + k);
+    float s32 = 0.0f, q32 = 0.0f;
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
       const int row = p * RP + lane / V4;
@@ -608,21 +667,16 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
         for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
         *(f32x4*)(adv + go) = av;
         *(f32x4*)(ret + go) = cur.v[p] + av;  // returns = values + advantages (ppo.py:241)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          lsum += (double)av[j];
-          lsq += (double)av[j] * (double)av[j];
-        }
+        stats4(av, s32, q32);
       }
     }
+    lsum += (double)s32;
+    lsq += (double)q32;
     GAE_STAMP(17 + k);
     cur = nxt;
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    lsum += __shfl_xor(lsum, off);
-    lsq += __shfl_xor(lsq, off);
-  }
+  lsum = wave_sum_f64(lsum);
+  lsq = wave_sum_f64(lsq);
   if (lane == 0) {
     L.wsum[k][0] = lsum;
     L.wsum[k][1] = lsq;
