@@ -164,11 +164,19 @@ def gae_roofline(device, T=128, N=8192, sets=None, reps=4, mode=0):
     torch.cuda.empty_cache()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "gae_aff_kernel<32>" if mode else "gae_pipe_kernel<32>",
+            "kernel": ("gae_aff_kernel<%d>" if mode else "gae_pipe_kernel<%d>") % _gae_tile(N),
             "mode": "affine (<= 1e-6 of scale)" if mode else "exact (bit-exact serial)",
             "num_envs": N, "rollout_steps": T,
             "bytes_per_launch": nbytes, "us_per_launch": round(per * 1e3, 2),
             "launches": cnt, "rotating_sets": sets}
+
+
+def _gae_tile(N):
+    """The env-tile width gae.hip's launcher picks for N (64 / 32 / 16 envs per workgroup)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    if N % 64 == 0 and N // 64 >= cus:
+        return 64
+    return 32 if N % 32 == 0 and N // 32 >= cus else 16
 
 
 def _baseline_inputs(cfg_name, seed=0):
