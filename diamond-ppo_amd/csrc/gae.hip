@@ -222,14 +222,25 @@ __device__ __forceinline__ float gae_carry(float delta, float coef, float a) {
 }
 
 // The normalisation statistics (ppo.py:243) of a row's 4 advantages, in fp32 and in a fixed
-// order; the caller adds one fp32 partial per chunk (<= 8 values) into its fp64 sums.  Per-value
-// fp64 accumulation cost 3 half-rate fp64 operations per value on the SIMD the scan runs on.
-__device__ __forceinline__ void stats4(const f32x4& av, float& s, float& q) {
+// order, shifted by the lane's first advantage of the chunk (sft): the caller adds one fp32
+// partial per chunk (<= 8 values) into its fp64 sums as sum x = S + n sft and
+// sum x^2 = Q + sft (2 S + n sft).  Per-value fp64 accumulation cost 3 half-rate fp64 operations
+// per value on the SIMD the scan runs on; unshifted fp32 partials lose the variance when the
+// advantages' mean dwarfs their spread (std off by 1.6e-5 at mean / std = 1,000; shifted 7e-9).
+__device__ __forceinline__ void stats4(const f32x4& av, float sft, float& s, float& q) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    s += av[j];
-    q = __builtin_fmaf(av[j], av[j], q);
+    const float dx = av[j] - sft;
+    s += dx;
+    q = __builtin_fmaf(dx, dx, q);
   }
+}
+
+__device__ __forceinline__ void stats_fold(float s32, float q32, float sft, int cnt, double& lsum,
+                                           double& lsq) {
+  const double ds = (double)sft, dn = (double)cnt, dsum = (double)s32;
+  lsum += dsum + dn * ds;
+  lsq += (double)q32 + ds * (2.0 * dsum + dn * ds);
 }
 
 template <int CTRL>
@@ -374,7 +385,8 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
         GAE_STAMP(1 + k);
         wait_flag(&L.scanned[k], gen);
         GAE_STAMP(9 + k);
-        float s32 = 0.0f, q32 = 0.0f;
+        float s32 = 0.0f, q32 = 0.0f, sft = 0.0f;
+        int cnt = 0;
         // every pass's advantages read before the first store: the write-through stores are asm
         // with a memory clobber, so reads placed after one wait for their own LDS round trip
         f32x4 avp[PER];
@@ -392,6 +404,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
           if (row < nr) {
             const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
             const f32x4 av = avp[p];
+            if (p == 0) sft = av[0];  // (a later pass has a row only if pass 0 has one)
             if (wt) {
               store_wt(adv + go, av);
               store_wt(ret + go, xv[p] + av);  // returns = values + advantages (ppo.py:241)
@@ -399,11 +412,11 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
               *(f32x4*)(adv + go) = av;
               *(f32x4*)(ret + go) = xv[p] + av;
             }
-            stats4(av, s32, q32);
+            stats4(av, sft, s32, q32);
+            cnt += 4;
           }
         }
-        lsum += (double)s32;
-        lsq += (double)q32;
+        stats_fold(s32, q32, sft, cnt, lsum, lsq);
         GAE_STAMP(17 + k);
       }
     }
@@ -656,7 +669,8 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
       if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
     }
     GAE_STAMP(33 + k);
-    float s32 = 0.0f, q32 = 0.0f;
+    float s32 = 0.0f, q32 = 0.0f, sft = 0.0f;
+    int cnt = 0;
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
       const int row = p * RP + lane / V4;
@@ -667,11 +681,12 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
         for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
         *(f32x4*)(adv + go) = av;
         *(f32x4*)(ret + go) = cur.v[p] + av;  // returns = values + advantages (ppo.py:241)
-        stats4(av, s32, q32);
+        if (p == 0) sft = av[0];
+        stats4(av, sft, s32, q32);
+        cnt += 4;
       }
     }
-    lsum += (double)s32;
-    lsq += (double)q32;
+    stats_fold(s32, q32, sft, cnt, lsum, lsq);
     GAE_STAMP(17 + k);
     cur = nxt;
   }

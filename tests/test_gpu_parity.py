@@ -94,6 +94,33 @@ def test_gae_vs_oracle_sizes(T, Nn):
         assert abs(ms[1] - std) <= 2e-6 * std
 
 
+@pytest.mark.parametrize("T,Nn,mode", [(128, 8192, 0), (128, 4096, 0), (128, 65536, 0),
+                                       (129, 33, 0), (64, 6144, 0), (300, 64, 0),
+                                       (128, 8192, 1), (128, 65536, 1)])
+def test_gae_stats_large_mean(T, Nn, mode):
+    """Normalisation statistics when the advantages' mean dwarfs their spread: every step terminal
+    (adv = r - v), v = -1,000, r ~ N(0, 1), so mean / std ~ 1,000 -- the case in which fp32
+    partial sums lose the variance (the kernels shift each lane's chunk by its first advantage).
+    Mean and std within 1e-6 / 2e-6 of the float64 oracle (P.adv_stats), the normalised
+    advantages within 2e-6 of P.normalize_adv; every kernel (32-, 16-, 64-env tiles, the
+    unaligned serial kernel, super-chunks, and the affine mode)."""
+    from oracle import ppo_np as P
+    rng = np.random.default_rng(T * 7 + Nn)
+    r = rng.standard_normal((T, Nn)).astype(np.float32)
+    te = np.ones((T, Nn), np.uint8)
+    tr = np.zeros((T, Nn), np.uint8)
+    v = np.full((T, Nn), -1000.0, np.float32)
+    nv = rng.standard_normal((T, Nn)).astype(np.float32)
+    adv, ret, ms, norm = run_gae(r, te, tr, v, nv, mode=N.GAE_AFFINE if mode else 0)
+    ref = P.gae(r, te, tr, v, nv)
+    if not mode:
+        assert np.array_equal(adv, ref)
+    mean, std = P.adv_stats(ref)
+    assert abs(ms[0] - mean) <= 1e-6 * abs(mean), (ms[0], mean)
+    assert abs(ms[1] - std) <= 2e-6 * std, (ms[1], std)
+    np.testing.assert_allclose(norm, P.normalize_adv(adv), rtol=0, atol=2e-6)
+
+
 @pytest.mark.parametrize("T,Nn", [(128, 8192), (128, 65536), (128, 4096), (300, 64),
                                   (129, 4096), (200, 8448), (64, 6144), (16, 12288), (1, 32),
                                   (100, 512), (7, 4104)])
