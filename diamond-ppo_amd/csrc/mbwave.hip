@@ -176,6 +176,23 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// The weight-gradient accumulation in AGPR form (accumulator read and written in place in the
+// AGPRs) while the rest of the file builds in VGPR form: the gradient tiles live in AGPRs across
+// the whole loop, and a VGPR-form MFMA on them needed them copied into VGPRs and back (the loop
+// of the CartPole instantiation: 326 AGPR reads -> 28).  Measured per launch: C2 55.5 -> 54.5 µs,
+// C3 100.9 -> 99.6; the Gaussian-head instantiations measured slower (C4 63.1 -> 64.6) and keep
+// the builtin.  DPPO_MBW_VGPR_WGRAD: the builtin everywhere (A/B).
+template <bool AGPR>
+__device__ __forceinline__ void mfma4_acc(float a, float b, f32x4& c) {
+#ifndef DPPO_MBW_VGPR_WGRAD
+  if constexpr (AGPR) {
+    asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+    return;
+  }
+#endif
+  c = mfma4(a, b, c);
+}
+
 __device__ __forceinline__ float tanh_w(float x) {
   // tanh = 1 - 2 / (e^{2x} + 1): five instructions (v_exp, v_rcp and three plain ones) beside a
   // wave's MFMAs; saturates to +-1 through e^{2x} = inf / 0, absolute error <= ~1.2e-7 (the
@@ -400,7 +417,7 @@ __device__ __forceinline__ void bwdP2(f32x4 (&t)[4], const float* W, const f32x4
 
 // dW tiles += dZ X^T over the group's 16 samples (both operands in P layout, or X in the natural
 // T layout of the input features for dW1).
-template <int NIB>
+template <int NIB, bool AGPR>
 __device__ __forceinline__ void wgrad(f32x4* acc, const f32x4 (&dzt)[4], const f32x4* xt) {
 #pragma unroll
   for (int v = 0; v < 4; ++v)
@@ -408,7 +425,7 @@ __device__ __forceinline__ void wgrad(f32x4* acc, const f32x4 (&dzt)[4], const f
     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
       for (int ib = 0; ib < NIB; ++ib)
-        acc[ob * NIB + ib] = mfma4(dzt[ob][v], xt[ib][v], acc[ob * NIB + ib]);
+        mfma4_acc<AGPR>(dzt[ob][v], xt[ib][v], acc[ob * NIB + ib]);
 }
 
 // N -> P through the wave's scratch (sample-major rows of kSm floats): 16-B writes of the N tiles,
@@ -596,6 +613,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   // (not in the 4-discrete-action instantiation, which has no registers to spare: its main loop
   // would spill)
   constexpr bool kTight = AMAX == 4 && !CONT && NIB == 1;
+  constexpr bool kAgprW = !CONT;  // weight-gradient MFMAs in AGPR form (mfma4_acc)
   const int fs = tid < H ? tid : 0;
   const int hs = (tid >= H && tid - H < a.A) ? tid - H : 0;
   float sWv = 0.f, sb1 = 0.f, sb2 = 0.f, sba = 0.f, sbc = 0.f, sbo = 0.f, sls = 0.f, sbv = 0.f;
@@ -1031,8 +1049,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
         gb2[b] += (dz2t[b][0] + dz2t[b][1]) + (dz2t[b][2] + dz2t[b][3]);
       }
       put_p(sx, dz2t, q, r);
-      wgrad<4>(gWa, dzat, h2t);
-      wgrad<4>(gWc, dzct, h2t);
+      wgrad<4, kAgprW>(gWa, dzat, h2t);
+      wgrad<4, kAgprW>(gWc, dzct, h2t);
     }
     PHASE_FENCE();
     WSTAMP(k, 7);
@@ -1055,14 +1073,14 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       }
       // the next group's layer 1 (sh1 is free once h1t is read: one wave's LDS ops run in order)
       if (kHoistL1 && k + 1 < nk) layer1(h1, g_nxt);
-      wgrad<4>(gW2, dz2t, h1t);
+      wgrad<4, kAgprW>(gW2, dz2t, h1t);
       f32x4 dz1t[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
         dz1t[b] = dh1[b] * (1.0f - h1t[b] * h1t[b]);
         gb1[b] += (dz1t[b][0] + dz1t[b][1]) + (dz1t[b][2] + dz1t[b][3]);
       }
-      wgrad<NB1>(gW1, dz1t, g_cur.xt);
+      wgrad<NB1, kAgprW>(gW1, dz1t, g_cur.xt);
       if (X1) {
         // g_cur.xt[1][v] = input 16 of sample 4q + v in every lane (columns past 16 clamp to it)
 #pragma unroll
@@ -1075,6 +1093,9 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     PHASE_FENCE();
     WSTAMP(k, 8);
   }
+  // the epilogue reads the gradient tiles with v_accvgpr_read: the hazard recognizer does not
+  // see the asm MFMAs that wrote them, so their wait states are inserted here
+  if (kAgprW) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #ifdef DPPO_PHASE_TRACE
   WEDGE(2, (long long)__builtin_amdgcn_s_memtime());
 #endif
