@@ -1,35 +1,40 @@
 #!/usr/bin/env python3
 """Benchmark: env-steps/s of GAE + PPO update (one learn()) on synthetic [128 x num_envs] buffers.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cartpole4096]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config lunar8192]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W [--config c5]
+
+``python bench.py --gpus N`` with N > 1 and no launcher around it starts the N ranks itself (one
+child torch.distributed.run job; the parent touches no GPU) and exits with the job's status; a
+launcher whose world size differs from ``--gpus`` is an error (exit 2).
 
 A "step" is one full PPO.learn() (reference diamond/ppo.py:224-287) over one rollout buffer
 already resident in HBM: old-policy eval, GAE, returns, advantage normalisation, E x M = 32
 minibatch {forward, loss, backward, clip, Adam} steps and the LR-scheduler step.  The minibatch
 permutations are drawn from the global NumPy RNG inside the step, bit-exactly as the reference.
 
-Default workload (BASELINE.json configs[1]): CartPole-shaped PPO, T = 128,
-num_envs = 4096 per GPU (weak scaling: each rank owns 4096 envs, the gradient is all-reduced
-over RCCL once per minibatch), obs_dim 4, 2 actions, hidden 64, E = 4, M = 8.  ``--config c5``
-is BASELINE configs[4] as a STRONG-scaling run: 65,536 envs in total split over the ranks
-(8,192 per GPU at 8); its ``update_steps_per_s`` (minibatch optimizer steps per second) is the
-quantity the north star's >= 6x-at-8-GPUs target is stated in.  Synthetic data: obs/next_obs ~
-N(0,1), rewards ~ N(1,1), term ~ Bern(0.02), trunc ~ Bern(0.005), uniform actions,
-default_rng(rank); random-init weights of the reference architecture.
+Default workload (BASELINE.json configs[2]): LunarLander-shaped PPO, T = 128,
+num_envs = 8192 per GPU -- the largest single-GPU configuration, and the north star's GAE size
+(weak scaling: each rank owns 8192 envs, the gradient is exchanged once per minibatch), obs_dim
+8, 4 actions, hidden 64, E = 4, M = 8.  ``--config c5`` is BASELINE configs[4] as a
+STRONG-scaling run: 65,536 envs in total split over the ranks (8,192 per GPU at 8); its
+``update_steps_per_s`` (minibatch optimizer steps per second) is the quantity the north star's
+>= 6x-at-8-GPUs target is stated in.  Synthetic data: obs/next_obs ~ N(0,1), rewards ~ N(1,1),
+term ~ Bern(0.02), trunc ~ Bern(0.005), uniform actions, default_rng(rank); random-init weights
+of the reference architecture.
 
 Rank 0 prints ONE JSON line.  ``value`` comes from a timed pass with nothing but the learn()
 work in the stream.  A second timed pass of the same K learns stamps every kernel with its own
 start/end HIP events (libdppo timing mode): ``kernels``, ``device_ms_per_step`` and ``roofline``
 (the dominant kernel by device time, its average launch duration, algorithmic FLOP per launch)
-come from it, never the throughput.  At N = 1 the line also carries ``configs_extra`` (C3
-LunarLander 8192, C4 HalfCheetah 4096 and C5's 65,536 envs on one GPU -- the strong-scaling
+come from it, never the throughput.  At N = 1 the line also carries ``configs_extra`` (C2
+CartPole 4096, C4 HalfCheetah 4096 and C5's 65,536 envs on one GPU -- the strong-scaling
 anchor), ``roofline_gae`` (the GAE kernel at num_envs = 8192 over 16 rotating buffer sets, 368 MB
 > the 256 MB Infinity Cache; ``roofline_gae_affine`` the tolerance-mode kernel, and
-``roofline_gae_65536`` both at C5's one-GPU 65,536 envs) and ``cpu_baseline``: the PyTorch-CPU restatement of the reference
-path (oracle/ppo_torch.py) timed for one full learn() on the host cores, with the NumPy oracle
-beside it as ``cpu_baseline_numpy``.
+``roofline_gae_65536`` both at C5's one-GPU 65,536 envs) and ``cpu_baseline``: the PyTorch-CPU
+restatement of the reference path (oracle/ppo_torch.py) timed for one full learn() of the
+headline workload on the host cores, with the NumPy oracle beside it as ``cpu_baseline_numpy``.
 """
 from __future__ import annotations
 
@@ -387,12 +392,39 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
     return res
 
 
+def spawn_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` (N > 1) without a torch.distributed launcher around it: start
+    the N ranks as ONE child ``torch.distributed.run`` job (the parent makes no GPU call, so no
+    exec-after-GPU-init and no device context in the parent) and relay its exit status; rank 0's
+    JSON line reaches stdout through the inherited descriptors."""
+    import socket
+    import subprocess
+    rehearse = os.environ.get("DPPO_BENCH_REHEARSE") == "1"
+    have = torch.cuda.device_count()    # counts devices without initialising HIP (this image)
+    if not rehearse and have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible (DPPO_BENCH_REHEARSE=1 "
+              f"rehearses N ranks on one GPU)", file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); without a torch.distributed launcher, N > 1 "
+                         "starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cartpole4096", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="lunar8192", choices=sorted(CONFIGS),
+                    help="default: BASELINE configs[2], LunarLander N = 8192 per GPU -- the "
+                         "largest single-GPU config (the north star's GAE size)")
     ap.add_argument("--global-minibatches", action="store_true",
                     help="N > 1: every rank processes its members of the reference's global "
                          "minibatches (cfg.global_minibatches) instead of local-union minibatches")
@@ -404,7 +436,13 @@ def main():
                     help="diagnostic: no per-kernel HIP events in the timed region (no roofline)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # DPPO_BENCH_REHEARSE=1: rehearse the N > 1 path on a one-GPU box -- every rank on GPU 0, a
@@ -455,7 +493,7 @@ def main():
         # the other BASELINE configs on this GPU (C3, C4), and C5's 65,536 global envs on ONE
         # GPU: the anchor of the configs[4] strong-scaling curve (`--config c5 --gpus N`)
         extra = {}
-        for name in ("lunar8192", "cheetah4096", "c5"):
+        for name in ("cartpole4096", "lunar8192", "cheetah4096", "c5"):
             if name == args.config:
                 continue
             r = run_config(name, 1, 0, None, device, min(args.steps, 10), 2)
@@ -472,6 +510,7 @@ def main():
         out["roofline_gae_65536"] = {"exact": gae_roofline(device, N=65536),
                                      "affine": gae_roofline(device, N=65536, mode=1)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the CPU path on the headline workload itself (c5's 65,536 envs: its 4,096-env shape)
         tb, nb = cpu_baselines(args.config if args.config != "c5" else "cartpole4096")
         out["cpu_baseline"] = tb
         out["cpu_baseline_numpy"] = nb

@@ -409,8 +409,10 @@ int loop_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s)
 }
 
 // Exchange numbers: the same sequence on every rank; 0 is skipped (the tagged words start as 0).
+// The buffers are double-buffered by parity (seq & 1), so consecutive numbers must alternate
+// parity: after 0xFFFFFFFF (odd) comes 2, not 1.
 unsigned next_xseq(dppo_handle* h) {
-  if (++h->xseq == 0u) ++h->xseq;
+  if (++h->xseq == 0u) h->xseq = 2u;
   return h->xseq;
 }
 
@@ -1381,6 +1383,10 @@ int dppo_peer_open(dppo_handle* h, int32_t nranks, int32_t rank, const unsigned 
   // rank, not when ranks share a device (their grids would wait on each other for CUs).
   const char* fz = std::getenv("DPPO_PEER_FUSED");
   h->xfused = !(flags & DPPO_PEER_SHARED_DEVICE) && !(fz && fz[0] == '0');
+  // DPPO_PEER_XSEQ0 (tests): the exchange number to count on from, e.g. just below the 32-bit
+  // wrap; every rank must set the same value
+  const char* x0 = std::getenv("DPPO_PEER_XSEQ0");
+  if (x0) h->xseq = (unsigned)std::strtoul(x0, nullptr, 0);
   h->xworld = nranks;
   h->nranks = nranks;
   h->rank = rank;
@@ -1429,48 +1435,108 @@ int dppo_peer_selftest(dppo_handle* h, void* stream) {
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t s = S(stream);
   const int W = h->xworld;
+  const int tri = W * (W + 1) / 2;
   const int64_t n = h->layout.total + 8;
-  // rank r contributes (r + 1) * (i % 7 + 1) (f32) and (r + 1) * 0.25 (f64): exact sums
+  // Exchange k (k = 0..3, both buffer parities twice, so every exchange after the first two
+  // overwrites non-zero words of an earlier one): rank r contributes (r + 1) (i % 7 + 1) + 1000 k
+  // in f32 -- exact sums tri (i % 7 + 1) + 1000 W k -- and exchange 0 also (r + 1) {0.25, -0.5}
+  // in f64.  Then, where the learn runs the gradient exchange inside reduce_adam_kernel (one GPU
+  // per rank), two launches of that kernel on a one-slab scratch gradient (r + 1) (i % 5 + 1) +
+  // 100 k, both parities: its tagged-word sum must come out exact as well.
   std::vector<float> hf((size_t)n);
-  for (int64_t i = 0; i < n; ++i) hf[i] = (float)((h->rank + 1) * (int)(i % 7 + 1));
-  double hd[2] = {(h->rank + 1) * 0.25, -(h->rank + 1) * 0.5};
+  double hd[2];
   float* df = nullptr;
   double* dd = nullptr;
+  float *slab = nullptr, *pm = nullptr, *grad = nullptr;
   DPPO_TRY(dalloc(&df, n));
   DPPO_TRY(dalloc(&dd, 2));
-  int rc = DPPO_OK;
+  const bool fused = h->xfused && h->radam_ok && h->ra_tags;
+  if (fused) {
+    DPPO_TRY(dalloc(&slab, h->slab_stride));
+    DPPO_TRY(dalloc(&pm, 3 * h->layout.total));
+    DPPO_TRY(dalloc(&grad, n));
+  }
   auto run = [&]() -> int {
-    DPPO_HIP_CHECK(hipMemcpyAsync(df, hf.data(), n * 4, hipMemcpyHostToDevice, s));
-    DPPO_HIP_CHECK(hipMemcpyAsync(dd, hd, 16, hipMemcpyHostToDevice, s));
-    DPPO_TRY(peer_allreduce(h, df, (size_t)n, false, s));
-    DPPO_TRY(peer_allreduce(h, dd, 2, true, s));
-    DPPO_HIP_CHECK(hipMemcpyAsync(hf.data(), df, n * 4, hipMemcpyDeviceToHost, s));
-    DPPO_HIP_CHECK(hipMemcpyAsync(hd, dd, 16, hipMemcpyDeviceToHost, s));
-    DPPO_HIP_CHECK(hipStreamSynchronize(s));
-    DPPO_TRY(device_status(h));
-    const int tri = W * (W + 1) / 2;
-    for (int64_t i = 0; i < n; ++i) {
-      if (hf[i] != (float)(tri * (int)(i % 7 + 1))) {
-        set_error("peer exchange self-test: element %lld is %g, expected %d", (long long)i,
-                  (double)hf[i], tri * (int)(i % 7 + 1));
+    // DPPO_PEER_SELFTEST_SKEW=r (tests): rank r contributes one wrong element to exchange 0, as
+    // a rank reading stale or incoherent peer memory would see it
+    const char* skew = std::getenv("DPPO_PEER_SELFTEST_SKEW");
+    const int skew_rank = skew ? std::atoi(skew) : -1;
+    for (int k = 0; k < 4; ++k) {
+      for (int64_t i = 0; i < n; ++i)
+        hf[i] = (float)((h->rank + 1) * (int)(i % 7 + 1) + 1000 * k);
+      if (k == 0 && skew_rank == h->rank) hf[3] += 1.0f;
+      DPPO_HIP_CHECK(hipMemcpyAsync(df, hf.data(), n * 4, hipMemcpyHostToDevice, s));
+      DPPO_TRY(peer_allreduce(h, df, (size_t)n, false, s));
+      if (k == 0) {
+        hd[0] = (h->rank + 1) * 0.25;
+        hd[1] = -(h->rank + 1) * 0.5;
+        DPPO_HIP_CHECK(hipMemcpyAsync(dd, hd, 16, hipMemcpyHostToDevice, s));
+        DPPO_TRY(peer_allreduce(h, dd, 2, true, s));
+        DPPO_HIP_CHECK(hipMemcpyAsync(hd, dd, 16, hipMemcpyDeviceToHost, s));
+      }
+      DPPO_HIP_CHECK(hipMemcpyAsync(hf.data(), df, n * 4, hipMemcpyDeviceToHost, s));
+      DPPO_HIP_CHECK(hipStreamSynchronize(s));
+      DPPO_TRY(device_status(h));
+      for (int64_t i = 0; i < n; ++i) {
+        const float want = (float)(tri * (int)(i % 7 + 1) + 1000 * W * k);
+        if (hf[i] != want) {
+          set_error("peer exchange self-test: exchange %d element %lld is %g, expected %g", k,
+                    (long long)i, (double)hf[i], (double)want);
+          return DPPO_ECOMM;
+        }
+      }
+      if (k == 0 && (hd[0] != tri * 0.25 || hd[1] != -tri * 0.5)) {
+        set_error("peer exchange self-test: f64 sums %g %g, expected %g %g", hd[0], hd[1],
+                  tri * 0.25, -tri * 0.5);
         return DPPO_ECOMM;
       }
     }
-    if (hd[0] != tri * 0.25 || hd[1] != -tri * 0.5) {
-      set_error("peer exchange self-test: f64 sums %g %g, expected %g %g", hd[0], hd[1],
-                tri * 0.25, -tri * 0.5);
-      return DPPO_ECOMM;
+    if (!fused) return DPPO_OK;
+    const int64_t P = h->layout.total;
+    DPPO_HIP_CHECK(hipMemsetAsync(pm, 0, 3 * P * sizeof(float), s));
+    for (int k = 0; k < 2; ++k) {
+      for (int64_t i = 0; i < n; ++i)
+        hf[i] = (float)((h->rank + 1) * (int)(i % 5 + 1) + 100 * k);
+      DPPO_HIP_CHECK(hipMemcpyAsync(slab, hf.data(), n * 4, hipMemcpyHostToDevice, s));
+      PeerArgs pa{};
+      for (int r = 0; r < W; ++r) pa.bufs[r] = h->xpeer[r];
+      pa.data_bytes = h->xcap * 8;
+      pa.world = W;
+      pa.rank = h->rank;
+      pa.seq = next_xseq(h);
+      pa.err = h->err_dev;
+      pa.timeout_ticks = h->xticks;
+      DPPO_TRY(launch_reduce_adam(slab, 1, h->slab_stride, P, grad, h->ra_tags, 0, 0, 0.f, 0,
+                                  next_radam_epoch(h), pm, pm + P, pm + 2 * P, 0.5f, -1e-3f, 1.f,
+                                  0.9f, 0.999f, 1e-5f, nullptr, 1.f, 1.f, 0.f, h->err_dev,
+                                  h->xticks, s, &pa));
+      DPPO_HIP_CHECK(hipMemcpyAsync(hf.data(), grad, n * 4, hipMemcpyDeviceToHost, s));
+      DPPO_HIP_CHECK(hipStreamSynchronize(s));
+      DPPO_TRY(device_status(h));
+      for (int64_t i = 0; i < n; ++i) {
+        const float want = (float)(tri * (int)(i % 5 + 1) + 100 * W * k);
+        if (hf[i] != want) {
+          set_error("peer exchange self-test: fused exchange %d element %lld is %g, expected %g",
+                    k, (long long)i, (double)hf[i], (double)want);
+          return DPPO_ECOMM;
+        }
+      }
     }
     return DPPO_OK;
   };
   // a peer that cannot see our buffer fails the test in seconds, not after the learn's bound
   const unsigned long long ticks = h->xticks;
   if (h->xticks > 1000000000ull) h->xticks = 1000000000ull;
-  rc = run();
+  const int rc = run();
   h->xticks = ticks;
   (void)hipStreamSynchronize(s);
   (void)hipFree(df);
   (void)hipFree(dd);
+  if (fused) {
+    (void)hipFree(slab);
+    (void)hipFree(pm);
+    (void)hipFree(grad);
+  }
   return rc;
 }
 

@@ -436,13 +436,17 @@ class NativeLearner:
         d.all_reduce(t, op=d.ReduceOp.MIN)
         return bool(t.item())
 
+    def _gpu_identity(self):
+        """(host, PCI domain, bus, device) of this rank's GPU: ranks with equal identities share
+        one device."""
+        pr = torch.cuda.get_device_properties(self.device)
+        return (socket.gethostname(), pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+
     def _init_peer(self, d, required: bool) -> bool:
         """Map every rank's exchange buffer and run one checked exchange; every rank keeps the
         peer exchange only if every rank succeeded (ranks must never disagree on the transport)."""
         h = self.handle
-        pr = torch.cuda.get_device_properties(self.device)
-        me = (h.peer_export(), (socket.gethostname(), pr.pci_domain_id, pr.pci_bus_id,
-                                pr.pci_device_id))
+        me = (h.peer_export(), self._gpu_identity())
         mine = [None] * self.world
         d.all_gather_object(mine, me)
         gpus = [m[1] for m in mine]
@@ -484,20 +488,26 @@ class NativeLearner:
             b = {"n": n, "obs_h": torch.empty((n, self.D), dtype=torch.float32).pin_memory(),
                  "obs_d": torch.empty((n, self.D), dtype=torch.float32, device=self.device),
                  "act_d": torch.empty(shp, dtype=dt, device=self.device),
-                 "act_h": torch.empty(shp, dtype=dt).pin_memory(), "counter": 0}
+                 "act_h": torch.empty(shp, dtype=dt).pin_memory()}
             self._act_bufs = b
         b["obs_h"].numpy()[:] = obs
         b["obs_d"].copy_(b["obs_h"], non_blocking=True)
         s = torch.cuda.current_stream(self.device)
         N.check(self.handle.lib.dppo_act_f32(self.handle.h, self.flat.flat.data_ptr(),
                                              b["obs_d"].data_ptr(), n, seed & (2 ** 64 - 1),
-                                             b["counter"], b["act_d"].data_ptr(), s.cuda_stream),
-                "dppo_act_f32")
-        b["counter"] += 1
+                                             self._next_act_counter(), b["act_d"].data_ptr(),
+                                             s.cuda_stream), "dppo_act_f32")
         b["act_h"].copy_(b["act_d"], non_blocking=True)
         s.synchronize()
         out = b["act_h"].numpy()
         return out.copy() if self.continuous else out.astype(np.int64)
+
+    def _next_act_counter(self) -> int:
+        """The Philox call counter of the action samplers: ONE sequence shared by act() and the
+        squashing sampler, so no two calls with the same seed reuse a noise draw."""
+        c = self.__dict__.get("_act_counter", 0)
+        self._act_counter = c + 1
+        return c
 
     def _act_squash(self, observations, seed, squash):
         if not self.continuous:
@@ -519,13 +529,11 @@ class NativeLearner:
         b["obs_h"].numpy()[:] = obs
         b["obs_d"].copy_(b["obs_h"], non_blocking=True)
         s = torch.cuda.current_stream(self.device)
-        # call counter of this sampler (one Philox draw per sample and call, as act())
-        counter = self.__dict__.setdefault("_sq_counter", 0)
         N.check(self.handle.lib.dppo_act_squash_f32(
             self.handle.h, self.flat.flat.data_ptr(), b["obs_d"].data_ptr(), n,
-            seed & (2 ** 64 - 1), counter, N.ptr(lo), N.ptr(hi), b["out_d"][0].data_ptr(),
-            b["out_d"][1].data_ptr(), s.cuda_stream), "dppo_act_squash_f32")
-        self._sq_counter += 1
+            seed & (2 ** 64 - 1), self._next_act_counter(), N.ptr(lo), N.ptr(hi),
+            b["out_d"][0].data_ptr(), b["out_d"][1].data_ptr(), s.cuda_stream),
+            "dppo_act_squash_f32")
         b["out_h"].copy_(b["out_d"], non_blocking=True)
         s.synchronize()
         out = b["out_h"].numpy()

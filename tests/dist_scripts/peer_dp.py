@@ -130,7 +130,57 @@ def run_agent(rank, world, out):
     L.close()
 
 
-def run(rank, world, port, kind, out):
+def run_dead(rank, world, out):
+    """Rank 1 stops exchanging after the self-test (it sleeps past DPPO_PEER_TIMEOUT_S, as a
+    hung or crashed peer would): rank 0's learn() must end with the peer-timeout error
+    (DPPO_ECOMM -> RuntimeError) within the timeout, and refuse every later call."""
+    import time
+    import torch
+    import diamond
+    import bench
+    from gpu_helpers import SpecEnvs
+    T, Nl, D, A = 32, 64, 4, 2
+    timeout = float(os.environ["DPPO_PEER_TIMEOUT_S"])
+    cfg = diamond.PPOConfig(rollout_steps=T, num_envs=Nl, verbose=False)
+    agent = diamond.PPO(None, cfg, envs=SpecEnvs(D, A, False))
+    L = agent._learner
+    assert L.world == world and L.peer
+    ro, _ = bench.synth_rollout(T, Nl, D, A, False, 0.02, 0.005, rank, agent.device)
+    torch.cuda.synchronize()
+    err, again, elapsed = "", "", 0.0
+    if rank == 0:
+        t0 = time.perf_counter()
+        try:
+            agent.learn_device(ro)
+            agent.learn_trace()          # synchronises: the sticky error surfaces here
+        except RuntimeError as e:
+            err = str(e)
+        elapsed = time.perf_counter() - t0
+        try:
+            agent.learn_device(ro)
+        except RuntimeError as e:
+            again = str(e)
+    else:
+        time.sleep(timeout + 4.0)
+    np.savez(out, err=err, again=again, elapsed=elapsed, timeout=timeout)
+    L.close()
+
+
+def run_selftest_fail(rank, world, out):
+    """DPPO_PEER_SELFTEST_SKEW=1: rank 1's self-test contribution is wrong, so the sums are wrong
+    on every rank; under DPPO_COMM=peer every rank's agent construction must raise."""
+    import diamond
+    from gpu_helpers import SpecEnvs
+    err = ""
+    try:
+        diamond.PPO(None, diamond.PPOConfig(rollout_steps=8, num_envs=16, verbose=False),
+                    envs=SpecEnvs(4, 2, False))
+    except RuntimeError as e:
+        err = str(e)
+    np.savez(out, err=err)
+
+
+def run(rank, world, port, kind, out, env=None):
     _paths()
     os.environ["LOCAL_RANK"] = "0"          # every rank on the one GPU
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -138,12 +188,14 @@ def run(rank, world, port, kind, out):
     os.environ["RANK"], os.environ["WORLD_SIZE"] = str(rank), str(world)
     os.environ["DPPO_COMM"] = "peer"
     os.environ["DPPO_PEER_TIMEOUT_S"] = "30"
+    os.environ.update(env or {})
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        (run_handle if kind == "handle" else run_agent)(rank, world, out)
+        {"handle": run_handle, "agent": run_agent, "dead": run_dead,
+         "selftest_fail": run_selftest_fail}[kind](rank, world, out)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -559,6 +559,21 @@ def _act_agent(continuous, D, A, Nn):
     return Agent(None, Cfg(rollout_steps=8, num_envs=Nn, verbose=False), envs=envs)
 
 
+def test_act_and_squash_samplers_share_one_call_counter():
+    """act() and the squashing sampler draw from ONE Philox call counter: with the same seed, a
+    squashed call followed by an unsquashed one uses distinct draws (rewinding the counter
+    reproduces the squashed call's u)."""
+    D, A, n = 17, 6, 4096
+    agent = _act_agent(True, D, A, 64)
+    obs = np.random.default_rng(5).standard_normal((n, D)).astype(np.float32)
+    u1, _ = agent._learner.act(obs, 99, squash=True)
+    u2 = agent._learner.act(obs, 99)
+    assert not np.array_equal(u1, u2)
+    agent._learner._act_counter -= 2
+    u3, _ = agent._learner.act(obs, 99, squash=True)
+    assert np.array_equal(u1, u3)
+
+
 def test_fused_actions_categorical_distribution():
     """dppo_act_f32 (rollout sampling, replaces get_actions ppo.py:73-82): deterministic per
     (seed, counter), and its empirical action frequencies for one observation repeated 2^17 times
@@ -571,7 +586,7 @@ def test_fused_actions_categorical_distribution():
     o = rng.standard_normal(D).astype(np.float32)
     obs = np.tile(o, (n, 1))
     a1 = agent._learner.act(obs, 1234)
-    agent._learner._act_bufs["counter"] -= 1
+    agent._learner._act_counter -= 1
     a2 = agent._learner.act(obs, 1234)
     a3 = agent._learner.act(obs, 1234)
     assert a1.dtype == np.int64 and np.array_equal(a1, a2) and not np.array_equal(a2, a3)

@@ -25,12 +25,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _spawn(kind, tmp_path, world=2):
+def _spawn(kind, tmp_path, world=2, env=None):
     from dist_scripts import peer_dp
     ctx = mp.get_context("spawn")
     port = _free_port()
     outs = [str(tmp_path / f"{kind}_r{r}.npz") for r in range(world)]
-    procs = [ctx.Process(target=peer_dp.run, args=(r, world, port, kind, outs[r]))
+    procs = [ctx.Process(target=peer_dp.run, args=(r, world, port, kind, outs[r], env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -56,6 +56,42 @@ def test_peer_exchange_two_ranks_learn_matches_single_gpu(tmp_path):
                                    rtol=2e-5, atol=2e-6, err_msg=f"grad norm, gmb={gmb}")
         np.testing.assert_allclose(r0[f"params{gmb}"], r0[f"single{gmb}"], rtol=0, atol=5e-6,
                                    err_msg=f"params, gmb={gmb}")
+
+
+@pytest.mark.timeout(300)
+def test_peer_exchange_across_the_sequence_wrap(tmp_path):
+    """The exchange numbers wrap at 2^32 (0 is reserved) and the buffers are double-buffered by
+    parity: counting on from 0xFFFFFFF0, the self-test and both learns cross the wrap and must
+    still give identical parameters on both ranks, equal to the world-1 learn."""
+    r0, r1 = _spawn("handle", tmp_path, env={"DPPO_PEER_XSEQ0": str(0xFFFFFFF0)})
+    for gmb in (0, 1):
+        assert np.array_equal(r0[f"params{gmb}"], r1[f"params{gmb}"]), gmb
+        np.testing.assert_allclose(r0[f"params{gmb}"], r0[f"single{gmb}"], rtol=0, atol=5e-6)
+
+
+@pytest.mark.timeout(300)
+def test_dead_peer_fails_loudly_within_the_timeout(tmp_path):
+    """A rank that stops exchanging (every peer wait is bounded by
+    DPPO_PEER_TIMEOUT_S): the surviving rank's learn() raises the peer-timeout error within the
+    timeout instead of hanging, later calls on its handle refuse, and both processes exit."""
+    r0, _ = _spawn("dead", tmp_path, env={"DPPO_PEER_TIMEOUT_S": "3"})
+    err, again = str(r0["err"]), str(r0["again"])
+    assert "peer exchange timed out" in err, err
+    assert "peer exchange timed out" in again, again
+    assert float(r0["elapsed"]) < float(r0["timeout"]) + 10.0, float(r0["elapsed"])
+
+
+@pytest.mark.timeout(300)
+def test_failing_peer_selftest_is_refused_on_every_rank(tmp_path):
+    """A self-test whose sums come out wrong on every rank (rank 1 contributes one wrong element:
+    DPPO_PEER_SELFTEST_SKEW) -- the ranks agree on the failure and, with the peer exchange
+    required (DPPO_COMM=peer), every agent construction raises; under DPPO_COMM=auto the same
+    agreement falls back to RCCL (tests/test_comm_agreement_cpu.py: RCCL refuses two ranks on
+    this box's one GPU)."""
+    rs = _spawn("selftest_fail", tmp_path, env={"DPPO_PEER_SELFTEST_SKEW": "1"})
+    assert "expected" in str(rs[0]["err"]) or "another rank failed" in str(rs[0]["err"])
+    for r in rs:
+        assert "peer exchange unavailable" in str(r["err"]), str(r["err"])
 
 
 @pytest.mark.timeout(300)
@@ -110,24 +146,42 @@ def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces():
         L.close()
 
 
-@pytest.mark.timeout(300)
-def test_bench_two_rank_rehearsal_line():
-    """bench.py's N > 1 path (torch.distributed.run, barrier + max-over-ranks timing, one JSON
-    line from rank 0) rehearsed on the box's one GPU: DPPO_BENCH_REHEARSE=1 puts both ranks on
-    GPU 0 with a gloo group and the peer exchange between them."""
+def _bench_line(cmd, timeout=280):
     import json
     import os
     import subprocess
-    import sys
     from conftest import ROOT
     env = dict(os.environ, DPPO_BENCH_REHEARSE="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
                MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2",
-           "--steps", "3", "--warmup", "1"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
-    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_rank_rehearsal_line():
+    """bench.py's N > 1 path under an explicit launcher (torch.distributed.run, barrier +
+    max-over-ranks timing, one JSON line from rank 0) rehearsed on the box's one GPU:
+    DPPO_BENCH_REHEARSE=1 puts both ranks on GPU 0 with a gloo group and the peer exchange
+    between them."""
+    import sys
+    d = _bench_line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                     "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                     f"--master-port={_free_port()}", "bench.py", "--gpus", "2", "--steps", "3",
+                     "--warmup", "1", "--config", "cartpole4096"])
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0
     assert d["config"]["exchange"] == "peer" and d["config"]["num_envs_total"] == 2 * 4096
     assert d["kernels"]["allreduce"]["launches"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_flag_starts_the_ranks_itself():
+    """``python bench.py --gpus 2`` with no launcher (how the driver may run its scaling
+    sweep): bench.py starts the two ranks itself and rank 0's line says n_gpus 2, on the default
+    headline workload (LunarLander, 8192 envs per rank)."""
+    import sys
+    d = _bench_line([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1"])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0
+    assert d["config"]["name"] == "lunar8192" and d["config"]["num_envs_total"] == 2 * 8192
+    assert d["config"]["exchange"] == "peer"

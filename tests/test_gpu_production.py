@@ -19,9 +19,10 @@ These tests run the production shapes:
   samples: 4 / 8 / 4 groups per wave), plus a ragged one (m % 32 != 0, workgroups with unequal step
   counts), through ``dppo_minibatch_grad_f32`` against the oracle's ``minibatch_loss_grads`` on the
   same sample records and indices (reference ppo.py:261-283, continuous_ppo.py:273-295);
+* one minibatch gradient at C5's one-GPU size (1,048,576 samples: 64 groups per wave);
 * a full ``learn()`` at intermediate sizes (depth 1-3, both kernels, discrete and continuous) and at the full
-  C2 size (nit = 8) against the oracle's ``learn`` with the same NumPy permutations
-  (ppo.py:224-287).
+  C2, C3 and C4 sizes (4 / 8 / 4 groups per wave) against the oracle's ``learn`` with the same
+  NumPy permutations (ppo.py:224-287, continuous_ppo.py:236-299).
 
 Tolerances.  At these sizes every gradient entry is a sum of 65,536-131,072 fp32 terms, so BOTH
 fp32 implementations (the kernel and the NumPy oracle) carry a summation error of order
@@ -55,6 +56,9 @@ from gpu_helpers import (H, SpecEnvs, dev, hparams, production_depth, random_par
     ("C4 cheetah", 128, 4096, 17, 6, True, 0),
     ("C2 ragged", 128, 4096, 4, 2, False, 77),
     ("C4 ragged", 128, 4096, 17, 6, True, 4093),
+    # BASELINE configs[4] on ONE GPU (bench configs_extra.c5): 1,048,576-sample minibatches, 64
+    # groups per wave accumulated in the wave's registers
+    ("C5 one GPU", 128, 65536, 4, 2, False, 0),
     ("7 discrete actions", 128, 4096, 6, 7, False, 0),
     ("3 Gaussian actions, 20 inputs", 128, 4096, 20, 3, True, 13),
 ])
@@ -197,6 +201,22 @@ def test_learn_full_c2_vs_oracle():
     wave of the sample-split kernel)."""
     mb = learn_vs_oracle(128, 4096, 4, 2, False, seed=0)
     assert production_depth(mb, 4, 2, False) == 4
+
+
+def test_learn_full_c3_vs_oracle():
+    """BASELINE configs[2], the bench headline: LunarLander PPO, T = 128, N = 8192 (mb 131,072:
+    eight groups per wave of the sample-split kernel), the full 32-step learn() against the
+    oracle's learn with the same NumPy permutations (ppo.py:224-287)."""
+    mb = learn_vs_oracle(128, 8192, 8, 4, False, seed=2)
+    assert production_depth(mb, 8, 4, False) == 8
+
+
+def test_learn_full_c4_vs_oracle():
+    """BASELINE configs[3]: HalfCheetah ContinuousPPO, T = 128, N = 4096 (mb 65,536: four groups
+    per wave of the X1 sample-split instantiation), the full 32-step learn() against the oracle's
+    learn (continuous_ppo.py:236-299)."""
+    mb = learn_vs_oracle(128, 4096, 17, 6, True, seed=3)
+    assert production_depth(mb, 17, 6, True) == 4
 
 
 # ---------------------------------------------------------------------------------------------

@@ -290,3 +290,21 @@ def test_agents_fail_loudly_without_gpu():
     envs = gym_stub.SyncVectorEnv([lambda: gym_stub.SyntheticEnv(4, 2)] * 8)
     with pytest.raises(RuntimeError, match="GPU"):
         diamond.PPO(None, diamond.PPOConfig(num_envs=8, verbose=False), envs=envs)
+
+
+def test_bench_refuses_a_world_that_differs_from_gpus():
+    """bench.py exits non-zero (2) when the ranks it would report differ from --gpus: under a
+    launcher with another world size, or asked for more GPUs than are visible (no GPU call is
+    made before either check)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    env.pop("DPPO_BENCH_REHEARSE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 2 and "launcher started 1 rank" in r.stderr, r.stderr[-2000:]
+    env.pop("WORLD_SIZE")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "64"], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 2 and "GPU(s) visible" in r.stderr, r.stderr[-2000:]
