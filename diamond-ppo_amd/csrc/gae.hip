@@ -534,11 +534,20 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
 // affine maps compose: over a 16-step chunk, a_j = b_j + p_j * a_end with b, p the chunk's local
 // scan from the identity (b = 0, p = 1 at its end).  So every chunk owner scans its own 16 steps
 // at once -- all 8 owners of a 128-step super-chunk in parallel, instead of one wave walking 128
-// dependent steps -- publishes its chunk map (B, P) = (b_0, p_0), and after ONE workgroup barrier
-// folds the maps of the later chunks (<= 7 dependent steps) into its carry and finishes its rows.
-// The chunk that ends the rollout is bit-exact (carry 0); elsewhere the re-association costs a few
-// ulp (the parity test bounds it at 1e-6 of the advantages' scale).  8 waves, one per chunk,
-// no scan wave, no stagger: every load of the tile goes out at once.
+// dependent steps -- and publishes its chunk map (B, P) = (b_0, p_0) in LDS with a per-chunk flag.
+// The owner of chunk k then waits ONLY for the maps of the later chunks j > k (no workgroup
+// barrier), folds them into the super-chunk's carry in the fixed order j = 7 .. k + 1 (<= 7
+// dependent steps: the same operations, so the same bits, whatever the arrival order), finishes
+// its 16 advantages and stores them at once -- stores leave chunk by chunk as the loads land.
+// The owners start their first loads staggered (wave w = chunk 7 - w, `stagger` cycles apart), as
+// in gae_pipe_kernel, so chunks land in the order the folds need them.  The chunk that ends the
+// rollout is bit-exact (carry 0); elsewhere the re-association costs a few ulp (the parity test
+// bounds it at 1e-6 of the advantages' scale).
+// Buffers reused across iterations (tile, super-chunk) are double-buffered by iteration parity,
+// with back-pressure where a writer could lap a reader: the owner of chunk k rewrites its map
+// slot only after every lower chunk's owner has read the map it holds (rdone), and the carry
+// slot (written by chunk 0's owner) is only rewritten after every owner published its next map.
+// DPPO_GAE_AFF_BARRIER: the round-3 form (one workgroup barrier per iteration; A/B timing).
 template <int E>
 struct AffLds {
   float delta[E][kPStride];  // env-major rows of this super-chunk (wave-private row ranges)
@@ -546,18 +555,30 @@ struct AffLds {
   float a[E][kPStride];
   float B[2][kPChunks][E];   // chunk maps, double-buffered by iteration parity
   float P[2][kPChunks][E];
-  float carry[2][E];         // advantage at the end of the current super-chunk
+  float carry[2][E];         // advantage at the start of the previous super-chunk
+  int mflag[kPChunks];       // iteration (gen) whose map chunk k's slot holds
+  int rdone[kPChunks];       // last iteration whose later-chunk maps chunk k's owner has read
+  int cflag;                 // last iteration whose carry-out chunk 0's owner has published
   double wsum[kPChunks][2];
 };
+
+__device__ __forceinline__ int lds_ld(const int* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// After a poll loop on LDS flags: keep the compiler from moving the LDS accesses that the flags
+// guard above the loop (the hardware performs one wave's LDS operations in order)
+__device__ __forceinline__ void after_poll() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
 
 template <int E>
 __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
     const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ val,
     const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
-    double* __restrict__ partials, int T, int N, float g, float c) {
+    double* __restrict__ partials, int T, int N, float g, float c, int stagger) {
   __shared__ __attribute__((aligned(16))) AffLds<E> L;
-  const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;  // wave k owns chunk k
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k = kPChunks - 1 - wave;     // wave w owns chunk 7 - w (the latest chunk loads first)
   const int ntiles = N / E;
   const int nsup = (T + kPSuper - 1) / kPSuper;
   constexpr int V4 = E / 4;              // lanes per row (4 envs each)
@@ -565,6 +586,12 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
   constexpr int PER = kPChunk / RP;      // passes per chunk
   const int e0 = 4 * (lane % V4);
   const int r0 = k * kPChunk;
+  if (threadIdx.x < kPChunks) {
+    L.mflag[threadIdx.x] = 0;
+    L.rdone[threadIdx.x] = 0;
+  }
+  if (threadIdx.x == 0) L.cflag = 0;
+  __syncthreads();
   // iterations q = (tile, super-chunk) pairs of this workgroup, super-chunks latest first
   const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   const int niter = my_tiles * nsup;
@@ -599,10 +626,14 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
   };
   double lsum = 0.0, lsq = 0.0;
   GAE_STAMP(0);
+  if (stagger > 0 && wave > 0) {
+    const long long until = (long long)__builtin_amdgcn_s_memtime() + (long long)wave * stagger;
+    while ((long long)__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(2);
+  }
   Ops cur{}, nxt{};
   if (niter > 0) load(0, cur);
   for (int q = 0; q < niter; ++q) {
-    const int par = q & 1;
+    const int par = q & 1, gen = q + 1;
     int64_t base;
     int lo, nr, s;
     geom(q, base, lo, nr, s);
@@ -626,6 +657,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
     // local scan of the chunk from the identity, lane = env (this wave's own LDS rows: its LDS
     // operations complete in order)
     float bl[kPChunk], pl[kPChunk];
+    float cin = 0.0f;
     if (lane < E) {
       f32x4 d4[4], c4[4];
 #pragma unroll
@@ -641,6 +673,9 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
         bl[j] = b;
         pl[j] = pp;
       }
+    }
+#ifdef DPPO_GAE_AFF_BARRIER
+    if (lane < E) {
       L.B[par][k][lane] = bl[0];
       L.P[par][k][lane] = pl[0];
     }
@@ -648,10 +683,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
     __syncthreads();
     GAE_STAMP(25 + k);
     if (lane < E) {
-      // the carry into this chunk: the later super-chunk's, then the later chunks' maps
-      float cin = s == 0 ? 0.0f : L.carry[par][lane];
-      // every map read first, then the <= 7 dependent steps (a rolled loop over j > k waited for
-      // each read: ~150 cycles per step)
+      cin = s == 0 ? 0.0f : L.carry[par][lane];
       float Bj[kPChunks], Pj[kPChunks];
 #pragma unroll
       for (int j = 0; j < kPChunks; ++j) {
@@ -661,6 +693,61 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
 #pragma unroll
       for (int j = kPChunks - 1; j > 0; --j)
         if (j > k) cin = gae_carry(Bj[j], Pj[j], cin);
+    }
+#else
+    // back-pressure: this map slot was last written for iteration q - 2; every lower chunk's
+    // owner must have read it (rdone) before it is overwritten
+    if (gen > 2) {
+      bool ok;
+      do {
+        ok = true;
+#pragma unroll
+        for (int j = 0; j < kPChunks; ++j)
+          if (j < k && lds_ld(&L.rdone[j]) < gen - 2) ok = false;
+        if (!ok) __builtin_amdgcn_s_sleep(1);
+      } while (!ok);
+      after_poll();
+    }
+    if (lane < E) {
+      L.B[par][k][lane] = bl[0];
+      L.P[par][k][lane] = pl[0];
+    }
+    if (lane == 0) set_flag(&L.mflag[k], gen);
+    GAE_STAMP(9 + k);
+    // the carry into the super-chunk (chunk 0's owner published it one iteration earlier)
+    if (s > 0) {
+      while (lds_ld(&L.cflag) < gen - 1) __builtin_amdgcn_s_sleep(1);
+      after_poll();
+    }
+    // the later chunks' maps: poll their flags, then read every map at once
+    {
+      bool ok;
+      do {
+        ok = true;
+#pragma unroll
+        for (int j = 0; j < kPChunks; ++j)
+          if (j > k && lds_ld(&L.mflag[j]) < gen) ok = false;
+        if (!ok) __builtin_amdgcn_s_sleep(1);
+      } while (!ok);
+      after_poll();
+    }
+    GAE_STAMP(25 + k);
+    if (lane < E) {
+      cin = s == 0 ? 0.0f : L.carry[par][lane];
+      float Bj[kPChunks], Pj[kPChunks];
+#pragma unroll
+      for (int j = 0; j < kPChunks; ++j) {
+        Bj[j] = j > k ? L.B[par][j][lane] : 0.0f;
+        Pj[j] = j > k ? L.P[par][j][lane] : 1.0f;
+      }
+      // the fold in the fixed order j = 7 .. k + 1: the same bits whatever the arrival order
+#pragma unroll
+      for (int j = kPChunks - 1; j > 0; --j)
+        if (j > k) cin = gae_carry(Bj[j], Pj[j], cin);
+    }
+    if (lane == 0) set_flag(&L.rdone[k], gen);   // (LDS operations of a wave complete in order)
+#endif
+    if (lane < E) {
       f32x4 av[4];
 #pragma unroll
       for (int j = 0; j < kPChunk; ++j) av[j >> 2][j & 3] = gae_carry(bl[j], pl[j], cin);
@@ -668,17 +755,27 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
       for (int qq = 0; qq < 4; ++qq) *(f32x4*)&L.a[lane][r0 + 4 * qq] = av[qq];
       if (k == 0) L.carry[par ^ 1][lane] = av[0][0];  // for the super-chunk before this one
     }
+#ifndef DPPO_GAE_AFF_BARRIER
+    if (k == 0 && lane == 0) set_flag(&L.cflag, gen);
+#endif
     GAE_STAMP(33 + k);
     float s32 = 0.0f, q32 = 0.0f, sft = 0.0f;
     int cnt = 0;
+    f32x4 avp[PER];
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      const int row = p * RP + lane / V4;
+      if (row < nr) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) avp[p][j] = L.a[e0 + j][r0 + row];
+      }
+    }
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
       const int row = p * RP + lane / V4;
       if (row < nr) {
         const int64_t go = base + (int64_t)row * N;
-        f32x4 av;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) av[j] = L.a[e0 + j][r0 + row];
+        const f32x4 av = avp[p];
         *(f32x4*)(adv + go) = av;
         *(f32x4*)(ret + go) = cur.v[p] + av;  // returns = values + advantages (ppo.py:241)
         if (p == 0) sft = av[0];
@@ -873,17 +970,17 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     if (e64) {
       if (mode == DPPO_GAE_AFFINE)
         DPPO_LAUNCH(gae_aff_kernel<64>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
-                    nv, adv, ret, partials, T, N, gamma, c);
+                    nv, adv, ret, partials, T, N, gamma, c, stagger);
       else
         DPPO_LAUNCH(gae_pipe_kernel<64>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
                     adv, ret, partials, T, N, gamma, c, wt, stagger);
     } else if (mode == DPPO_GAE_AFFINE) {
       if (e32)
         DPPO_LAUNCH(gae_aff_kernel<32>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
-                    nv, adv, ret, partials, T, N, gamma, c);
+                    nv, adv, ret, partials, T, N, gamma, c, stagger);
       else
         DPPO_LAUNCH(gae_aff_kernel<16>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
-                    nv, adv, ret, partials, T, N, gamma, c);
+                    nv, adv, ret, partials, T, N, gamma, c, stagger);
     } else if (e32)
       DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
                   adv, ret, partials, T, N, gamma, c, wt, stagger);

@@ -20,7 +20,7 @@ def _listing(tmp_path, body):
     for ln in body:
         if ln.startswith("asm "):
             lines += ["\t;;#ASMSTART", "\t" + ln[4:], "\t;;#ASMEND"]
-        elif ln.endswith(":"):
+        elif ln.startswith("."):
             lines.append(ln)
         else:
             lines.append("\t" + ln)
@@ -55,7 +55,8 @@ def test_srcc_overwritten_too_early(tmp_path):
 
 
 def test_hazard_across_loop_back_edge(tmp_path):
-    body = [".LBB0_1:", "v_accvgpr_read_b32 v9, a2", "s_nop 7", "s_nop 7",
+    body = [".LBB0_1:   ; =>This Inner Loop Header: Depth=1", "v_accvgpr_read_b32 v9, a2",
+            "s_nop 7", "s_nop 7",
             "asm " + MFMA.format(a="v5", b="v4"), "s_cbranch_scc1 .LBB0_1"]
     assert _listing(tmp_path, body) == ["R2"]
     body = [".LBB0_1:", "s_nop 7", "s_nop 3", "v_accvgpr_read_b32 v9, a2",

@@ -55,7 +55,7 @@ def main():
         t = buf[w] - buf[w][0]
         print(f"workgroup {0 if w == 0 else 128}: end {t[41]} cycles")
         if a.affine:
-            print("  chunk  loads-landed  local-scan-done  barrier-passed  fold-done  "
+            print("  chunk  loads-landed  map-published  later-maps-seen  fold-done  "
                   "stores-issued")
             for k in range(7, -1, -1):
                 print(f"  {k:5d}  {t[1 + k]:12d}  {t[9 + k]:15d}  {t[25 + k]:14d}  "

@@ -62,14 +62,14 @@ def parse(path, pat=""):
         if s == ";;#ASMEND":
             in_asm = False
             continue
-        if not s or s.startswith(";"):
+        s = s.split(";")[0].strip()      # trailing comments (";  =>This Inner Loop Header")
+        if not s:
             continue
         if s.endswith(":") and not s.startswith("s_"):
             kernels[cur].append(("label", s[:-1]))
             continue
         if s.startswith("."):
             continue
-        s = s.split(";")[0].strip()
         kernels[cur].append(("ins", s, in_asm))
     return kernels
 
