@@ -706,6 +706,8 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
         Timed tm(h, K_RADAM, s);
 #ifdef DPPO_ABL_RADAM_G1
         const int Gr = 1;  // timing-only ablation: the fixed cost of the launch without slab reads
+#elif defined(DPPO_ABL_HALF_SLABS)
+        const int Gr = (G + 1) / 2;  // timing-only: half the slab bytes (mbwave.hip ablation)
 #else
         const int Gr = G;
 #endif

@@ -1101,6 +1101,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #endif
 
   // ---------------- epilogue: the four waves' partials summed in LDS in a fixed order
+#ifdef DPPO_ABL_HALF_SLABS
+  // timing-only ablation (wrong results): the workgroups b with b & 8 -- the same-XCD partners
+  // b - 8 under round-robin dispatch -- skip the epilogue entirely, the best case of handing
+  // their partial slab to the partner (no LDS sum, no hand-off, no stores): the upper bound of
+  // what a pairwise slab reduction could save in this kernel
+  if (blockIdx.x & 8) return;
+#endif
   float* slab = a.slabs + (int64_t)blockIdx.x * a.slab_stride;
   float* stg0 = lds;
   float* stg1 = lds + kWavesW * kMat;
