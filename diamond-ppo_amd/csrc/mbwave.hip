@@ -728,9 +728,12 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int tb = 0; tb < NIB; ++tb)
         w1[ob][tb] = *(const f32x4*)(lds + L.W1 + ((16 * ob + r) * 4 + q) * 4 * NIB + 4 * tb);
+    // (X1: exactly 17 inputs, 5 k-steps known at compile time -- no run-time branch between the
+    // k-steps, so their MFMAs and LDS waits interleave)
+    const int nkn = X1 ? 5 : a.nkn;
 #pragma unroll
     for (int t = 0; t < 4 * NIB; ++t) {
-      if (t < a.nkn) {
+      if (t < nkn) {
 #pragma unroll
         for (int ob = 0; ob < 4; ++ob) h[ob] = mfma4(w1[ob][t >> 2][t & 3], g.xn[t], h[ob]);
       }
@@ -863,11 +866,30 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     f32x4 a1t[4], c1t[4];
     get_p(a1t, sx, q, r);
     get_p(c1t, sy, q, r);
-    float vpart = 0.f;
+    // Gaussian heads: the loss phase's constants (1 / (2 var), 1 / var, 1 / sigma per action; the
+    // entropy and log-prob-constant sums) as ONE batch of LDS reads here -- read at their use,
+    // each was an exposed LDS round trip inside the dependent loss chain (~10 per group)
+    constexpr int NG4 = CONT ? (AMAX + 3) / 4 : 1;
+    f32x4 kg[3][NG4], kent = z4();
+    if (CONT) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int c = 0; c < NG4; ++c) kg[i][c] = *(const f32x4*)(lds + L.gc + 8 * i + 4 * c);
+      kent = *(const f32x4*)(lds + L.gent);
+    }
+    auto kgc = [&](int i, int h) { return CONT ? kg[i][h >> 2][h & 3] : 0.f; };
+    // the value head's rows and bias in the same batch (without kPreHeads they were read one
+    // row at a time, each waited for right before its dot product)
+    f32x4 wvb[4];
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
-      vpart += dot4(kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q), c1[ob]);
-    const float val = qsum(vpart) + lds[L.bv];
+      wvb[ob] = kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q);
+    const float kbv = lds[L.bv];
+    float vpart = 0.f;
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) vpart += dot4(wvb[ob], c1[ob]);
+    const float val = qsum(vpart) + kbv;
     // ---- (5) per-sample loss and head deltas (ppo.py:264-280)
     const f32x4 sc = g_cur.sc;
     const float adv = sc[2], ret = sc[3];
@@ -878,10 +900,10 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int h = 0; h < AMAX; ++h) {
         const float d = g_cur.ca[h >> 2][h & 3] - out[h];
-        qq += (d * d) * lds[L.gc + h];  // 1 / (2 var): 0 past A
+        qq += (d * d) * kgc(0, h);  // 1 / (2 var): 0 past A
       }
-      logp = -qq - lds[L.gent + 1];
-      ent = lds[L.gent];
+      logp = -qq - kent[1];
+      ent = kent[0];
     } else {
       const int actn = __float_as_int(sc[0]);
       float mx = out[0];
@@ -920,8 +942,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     for (int h = 0; h < AMAX; ++h) {
       if (CONT) {
         const float dd = g_cur.ca[h >> 2][h & 3] - out[h];
-        const float zz = dd * lds[L.gc + 16 + h];
-        dl[h] = h < a.A ? dlogp * dd * lds[L.gc + 8 + h] : 0.f;
+        const float zz = dd * kgc(2, h);
+        dl[h] = h < a.A ? dlogp * dd * kgc(1, h) : 0.f;
         if (q == 0 && h < a.A) gls[h] += dlogp * (zz * zz - 1.0f);
       } else {
         const int actn = __float_as_int(sc[0]);
@@ -952,13 +974,36 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       dh2_pre[0] = bwdP_row(Wa, 0, q, r);
       dh2_pre[1] = bwdP_row(Wa, 1, q, r);
     }
+    // 5-8 heads: every LDS operand of this phase as one batch at its start -- the head deltas
+    // of the lane's four samples, the head rows of Wo^T dl, the value-head rows -- then a
+    // scheduling fence so that none of them sinks to its use (read there, each was an exposed LDS
+    // round trip in front of its MFMA: 12 per group)
+    float drv[4], dvv[4], woA[2][4];
+    f32x4 wvc[4];
+    if (kMfmaHeads) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        drv[v] = sd[kSdw * (4 * q + v) + (r < AMAX ? r : 0)];
+        dvv[v] = sd[kSdw * (4 * q + v) + kDv];
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int ob = 0; ob < 4; ++ob) woA[ks][ob] = lds[L.Wo + (4 * ks + q) * H + 16 * ob + r];
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+        wvc[ob] = kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q);
+      SG_FENCE();
+    }
     {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         if (kMfmaWo) {
           // A operand: the delta of head r of sample 4q + v (rows past the heads are zero)
-          const float dr = sd[kSdw * (4 * q + v) + (r < AMAX ? r : 0)] * (r < AMAX ? 1.f : 0.f);
-          const float dvs = sd[kSdw * (4 * q + v) + kDv];
+          const float dr = (kMfmaHeads ? drv[v]
+                                       : sd[kSdw * (4 * q + v) + (r < AMAX ? r : 0)]) *
+                           (r < AMAX ? 1.f : 0.f);
+          const float dvs = kMfmaHeads ? dvv[v] : sd[kSdw * (4 * q + v) + kDv];
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb) {
             gWoT[cb] = mfma4(dr, a1t[cb][v], gWoT[cb]);
@@ -990,8 +1035,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       f32x4 da = z4();
       if (kMfmaHeads) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          da = mfma4(lds[L.Wo + (4 * ks + q) * H + 16 * ob + r], bsel[ks], da);
+        for (int ks = 0; ks < 2; ++ks) da = mfma4(woA[ks][ob], bsel[ks], da);
       } else {
 #pragma unroll
         for (int h = 0; h < AMAX; ++h)
@@ -999,7 +1043,9 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
                            : *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q)) * dl[h];
       }
       dza[ob] = da * (1.0f - a1[ob] * a1[ob]);
-      dzc[ob] = ((kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q)) * dv) *
+      dzc[ob] = ((kMfmaHeads ? wvc[ob]
+                             : (kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q))) *
+                 dv) *
                 (1.0f - c1[ob] * c1[ob]);
     }
     put_n(sx, dza, q, r);
