@@ -461,8 +461,12 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
                         h->ret, h->partials, d.rollout_steps, d.num_envs, hp->gamma,
                         hp->gae_lambda, s, &h->n_partials, h->gae_mode));
   }
-  // (4) advantage statistics, global over ranks (ppo.py:243)
-  if (hp->advantage_norm) {
+  // (4) advantage statistics, global over ranks (ppo.py:243).  One rank: the pack kernel reduces
+  // the GAE partials itself (one launch and one kernel boundary fewer per learn); several: the
+  // reduced sums are all-reduced first.  DPPO_STATS_LAUNCH=1 keeps the separate launch (A/B).
+  static const bool stats_launch = std::getenv("DPPO_STATS_LAUNCH") != nullptr;
+  const bool fold_stats = hp->advantage_norm && !distributed(h) && !stats_launch;
+  if (hp->advantage_norm && !fold_stats) {
     {
       Timed tm(h, K_STATS, s);
       DPPO_TRY(launch_stats_reduce(h->partials, h->n_partials, h->dsum, s));
@@ -480,6 +484,8 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
   pa.adv = h->adv;
   pa.ret = h->ret;
   pa.dsum = h->dsum;
+  pa.partials = fold_stats ? h->partials : nullptr;
+  pa.n_partials = h->n_partials;
   pa.n_total = (double)h->B * (double)world_of(h);
   pa.advantage_norm = hp->advantage_norm;
   pa.adv_out = h->adv_n;

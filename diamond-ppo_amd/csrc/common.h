@@ -89,6 +89,11 @@ struct PackArgs {
   const float* adv;       // [B] raw advantages
   const float* ret;       // [B]
   const double* dsum;     // {sum, sumsq} of raw advantages (global), or null if no norm
+  // single rank: the GAE kernel's per-workgroup {sum, sumsq} partials, reduced by every pack
+  // block itself (the same fixed order as stats_reduce_kernel) instead of by a launch of its
+  // own; null -> dsum (multi-rank: dsum holds the all-reduced sums)
+  const double* partials;
+  int n_partials;
   double n_total;         // global sample count for the statistics
   int advantage_norm;
   float* adv_out;         // optional [B]: the (normalised) advantages handed to the update

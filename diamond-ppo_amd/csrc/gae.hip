@@ -806,10 +806,9 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
   }
 }
 
-// Sum the per-tile partials in a fixed order: dsum = {sum, sumsq}.
-__global__ __launch_bounds__(256) void stats_reduce_kernel(const double* __restrict__ partials,
-                                                           int n, double* __restrict__ dsum) {
-  __shared__ double s0[256], s1[256];
+// Sum the per-tile partials in a fixed order (256 threads): {sum, sumsq} in s0[0], s1[0].
+__device__ __forceinline__ void partials_sum256(const double* __restrict__ partials, int n,
+                                                double* s0, double* s1) {
   double a = 0.0, b = 0.0;
   for (int k = threadIdx.x; k < n; k += 256) {
     a += partials[2 * k];
@@ -825,6 +824,13 @@ __global__ __launch_bounds__(256) void stats_reduce_kernel(const double* __restr
     }
     __syncthreads();
   }
+}
+
+// dsum = {sum, sumsq} of the per-tile partials.
+__global__ __launch_bounds__(256) void stats_reduce_kernel(const double* __restrict__ partials,
+                                                           int n, double* __restrict__ dsum) {
+  __shared__ double s0[256], s1[256];
+  partials_sum256(partials, n, s0, s1);
   if (threadIdx.x == 0) {
     dsum[0] = s0[0];
     dsum[1] = s1[0];
@@ -863,6 +869,7 @@ __global__ void adv_normalize_kernel(float* __restrict__ adv, const float* __res
 // storing it per thread scattered 16-B pieces over every line and doubled the written bytes).
 constexpr int kPackTile = 256;
 
+static_assert(kPackTile == 256, "pack_kernel reduces the statistics with 256 threads");
 __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
   extern __shared__ __attribute__((aligned(16))) float pk_lds[];
   float* obs_s = pk_lds;                          // [256][D]
@@ -871,7 +878,16 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
   float mean = 0.0f, denom = 1.0f;
   if (a.advantage_norm) {
     float sd;
-    mean_std_from(a.dsum, a.n_total, &mean, &sd);
+    if (a.partials) {
+      // the statistics launch folded in: every block reduces the GAE partials itself, in
+      // stats_reduce_kernel's order (the same bits in every block and as the separate launch)
+      __shared__ double s0[kPackTile], s1[kPackTile];
+      partials_sum256(a.partials, a.n_partials, s0, s1);
+      const double ds[2] = {s0[0], s1[0]};
+      mean_std_from(ds, a.n_total, &mean, &sd);
+    } else {
+      mean_std_from(a.dsum, a.n_total, &mean, &sd);
+    }
     denom = sd + 1e-6f;
   }
   const int t = threadIdx.x;
