@@ -1335,6 +1335,15 @@ int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
     const int64_t bytes = (peer_buffer_bytes(cap) + (2 << 20) - 1) / (2 << 20) * (2 << 20);
     DPPO_TRY(dalloc(&h->xbuf, bytes));
     DPPO_HIP_CHECK(hipMemset(h->xbuf, 0, (size_t)bytes));
+    // DPPO_PEER_XSEQ0 (tests, dppo_peer_open): counting on from s0, the slice flags start as if
+    // exchange s0 had just completed -- the (wrap-safe) flag comparison needs flags within 2^31
+    // of the sequence, as they always are once exchanges have run
+    if (const char* x0 = std::getenv("DPPO_PEER_XSEQ0")) {
+      const unsigned s0 = (unsigned)std::strtoul(x0, nullptr, 0);
+      for (int k = 0; k < kPeerMaxSlices; ++k)
+        DPPO_HIP_CHECK(hipMemcpy(h->xbuf + 4 * cap * 8 + 64 * (int64_t)k, &s0, sizeof(s0),
+                                 hipMemcpyHostToDevice));
+    }
     DPPO_HIP_CHECK(hipDeviceSynchronize());
     h->xcap = cap;
   }
