@@ -18,6 +18,20 @@
     }                                                                                     \
   } while (0)
 
+// Raise a kernel's dynamic-LDS limit to what a CU has left beside the kernel's static LDS (a
+// request past 160 KiB in total fails, and a failed hipFuncSetAttribute leaves its error for the
+// next hipGetLastError -- i.e. the next launch check).  Callers run it once per process through a
+// function-local static initialiser, so concurrent launching threads (loopback groups) all wait
+// for it instead of racing past a half-set limit.
+inline void raise_dyn_lds(const void* fn) {
+  hipFuncAttributes at{};
+  size_t stat = 0;
+  if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(160 * 1024 - stat));
+  (void)hipGetLastError();
+}
+
 #define DPPO_LAUNCH_CHECK()                                                               \
   do {                                                                                    \
     hipError_t e_ = hipGetLastError();                                                    \

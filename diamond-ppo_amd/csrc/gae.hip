@@ -1036,12 +1036,12 @@ int launch_adv_normalize(float* adv, const float* mean_std, int64_t n, hipStream
 int launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.B <= 0) return DPPO_OK;
   const size_t lds = (size_t)kPackTile * (a.D + (a.continuous ? a.A : 0) + a.R) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {  // up to 100 KB at D = 32, A = 16
-    attr = true;
-    (void)hipFuncSetAttribute((const void*)pack_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  }
+  // up to 100 KB at D = 32, A = 16
+  static const bool attr = [] {
+    raise_dyn_lds((const void*)pack_kernel);
+    return true;
+  }();
+  (void)attr;
   DPPO_LAUNCH(pack_kernel, dim3(grid_for(a.B, kPackTile)), dim3(kPackTile), lds, s, a);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;

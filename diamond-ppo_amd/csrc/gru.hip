@@ -744,12 +744,11 @@ int dppo_gru_minibatch_grad_f32(dppo_gru_handle* h, const float* params,
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
-  static bool attr = false;
-  if (!attr) {
-    attr = true;
-    (void)hipFuncSetAttribute((const void*)gru_grad_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  }
+  static const bool attr = [] {
+    raise_dyn_lds((const void*)gru_grad_kernel);
+    return true;
+  }();
+  (void)attr;
   const dppo_gru_dims& d = h->dims;
   int rc = launch_gru_grad(h->po, params, *batch, idx, m, h->wmask, h->B, d.rollout_steps,
                            d.num_envs, d.obs_dim, d.act_dim, (float)(1.0 / (double)m_total),

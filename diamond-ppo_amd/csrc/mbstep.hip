@@ -1190,16 +1190,14 @@ int launch_mb(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, in
     set_error("fused minibatch kernel needs %zu bytes of LDS (> 160 KiB)", lds);
     return DPPO_EUNSUPPORTED;
   }
-  static bool attr = false;
-  if (!attr) {
-    attr = true;
-#define DPPO_SET2(A, C)                                                                       \
-  (void)hipFuncSetAttribute((const void*)mb_kernel<A, C>,                                     \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const bool attr = [] {
+#define DPPO_SET2(A, C) raise_dyn_lds((const void*)mb_kernel<A, C>);
     DPPO_SET2(2, false) DPPO_SET2(2, true) DPPO_SET2(4, false) DPPO_SET2(4, true)
     DPPO_SET2(8, false) DPPO_SET2(8, true) DPPO_SET2(16, false) DPPO_SET2(16, true)
 #undef DPPO_SET2
-  }
+    return true;
+  }();
+  (void)attr;
   const dim3 grid((unsigned)G), block(kThreads);
   const bool c = sh.continuous != 0;
   if (sh.A <= 2) {

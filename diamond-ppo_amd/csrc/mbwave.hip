@@ -1410,19 +1410,16 @@ int launch_mbw(const MlpShape& sh, const ParamOffsets& po, const GradArgs& ga, i
     set_error("minibatch kernel needs %zu bytes of LDS (> 160 KiB)", lds);
     return DPPO_EUNSUPPORTED;
   }
-  static bool attr = false;
-  if (!attr) {
-    attr = true;
-#define DPPO_SETW(A, C, N)                                                                    \
-  (void)hipFuncSetAttribute((const void*)mbw_kernel<A, C, N>,                                 \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const bool attr = [] {
+#define DPPO_SETW(A, C, N) raise_dyn_lds((const void*)mbw_kernel<A, C, N>);
     DPPO_SETW(2, false, 1) DPPO_SETW(2, true, 1) DPPO_SETW(4, false, 1) DPPO_SETW(4, true, 1)
     DPPO_SETW(2, false, 2) DPPO_SETW(2, true, 2) DPPO_SETW(4, false, 2) DPPO_SETW(4, true, 2)
     DPPO_SETW(8, false, 1) DPPO_SETW(6, true, 2)
-    (void)hipFuncSetAttribute((const void*)mbw_kernel<6, true, 2, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 #undef DPPO_SETW
-  }
+    raise_dyn_lds((const void*)mbw_kernel<6, true, 2, true>);
+    return true;
+  }();
+  (void)attr;
   const dim3 grid((unsigned)G), block(kThreadsW);
   const bool c = sh.continuous != 0;
   const bool n2 = D16 > 16;

@@ -670,24 +670,19 @@ KArgs base_args(const MlpShape& sh, const ParamOffsets& po, const float* params)
   } while (0)
 
 void raise_lds_limits() {
-  static bool done = false;
-  if (done) return;
-  done = true;
-  const size_t mx = 160 * 1024;
-#define DPPO_SET(A, C)                                                                  \
-  (void)hipFuncSetAttribute((const void*)eval_kernel<A, C>,                             \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
-  DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
-  DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
+  static const bool done = [] {
+#define DPPO_SET(A, C) raise_dyn_lds((const void*)eval_kernel<A, C>);
+    DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
+    DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
 #undef DPPO_SET
-  (void)hipFuncSetAttribute((const void*)next_eval_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
-#define DPPO_SET(A, C)                                                                  \
-  (void)hipFuncSetAttribute((const void*)act_kernel<A, C>,                              \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
-  DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
-  DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
+    raise_dyn_lds((const void*)next_eval_kernel);
+#define DPPO_SET(A, C) raise_dyn_lds((const void*)act_kernel<A, C>);
+    DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
+    DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
 #undef DPPO_SET
+    return true;
+  }();
+  (void)done;
 }
 
 int cu_count() {

@@ -421,8 +421,11 @@ int reduce_adam_capacity(int device, int64_t p_total) {
 int launch_fanin_probe(int blocks, int lds_bytes, unsigned* ctr, unsigned* err,
                        unsigned long long timeout_ticks, hipStream_t s) {
   if (lds_bytes < 4) lds_bytes = 4;
-  (void)hipFuncSetAttribute((const void*)fanin_probe_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const bool attr = [] {
+    raise_dyn_lds((const void*)fanin_probe_kernel);
+    return true;
+  }();
+  (void)attr;
   DPPO_LAUNCH(fanin_probe_kernel, dim3((unsigned)blocks), dim3(1024), (size_t)lds_bytes, s, ctr,
               err, timeout_ticks);
   DPPO_LAUNCH_CHECK();

@@ -77,8 +77,8 @@ def run_loopback(T, Nl, D, A, cont, E, M, flat0, host, perms, global_mb):
     for x in th:
         x.join(timeout=240)
     assert all(not x.is_alive() for x in th)
-    for r, x in enumerate(state):
-        assert x["rc"] == 0, (r, x["rc"], x["err"])
+    bad = [(r, x["rc"], x["err"]) for r, x in enumerate(state) if x["rc"] != 0]
+    assert not bad, bad
     torch.cuda.synchronize()
     out = [(x["p"].cpu().numpy(), handles[r].trace(E * M)) for r, x in enumerate(state)]
     for h in handles:
