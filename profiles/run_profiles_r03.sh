@@ -8,7 +8,7 @@
 # CONFIGS / GAES (|-separated, empty = none) select the runs.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$R/gpurun_out/prof3
+OUT=${PROF_OUT:-$R/gpurun_out/prof3}
 mkdir -p $OUT
 cd /tmp
 export TMPDIR=/tmp
