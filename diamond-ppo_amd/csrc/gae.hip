@@ -181,9 +181,19 @@ __device__ long long g_gae_trace[2][48];
         (slot != 0 || threadIdx.x == 0) && (slot != 41 || threadIdx.x == 0))          \
       g_gae_trace[blockIdx.x ? 1 : 0][slot] = __builtin_amdgcn_s_memtime();            \
   } while (0)
+// the "loads landed" stamps (1 + k) first wait for the chunk's loads and LDS writes: s_memtime has
+// no data dependency, so without the wait it can issue before the data it is meant to time
+#define GAE_STAMP_LANDED(slot)                                      \
+  do {                                                              \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");     \
+    GAE_STAMP(slot);                                                \
+  } while (0)
 #else
 #define GAE_STAMP(slot) \
   do {                  \
+  } while (0)
+#define GAE_STAMP_LANDED(slot) \
+  do {                         \
   } while (0)
 #endif // env-major rows: 16-B aligned, conflict-free b128 reads
 
@@ -382,7 +392,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
           }
         }
         if (lane == 0) set_flag(&L.loaded[k], gen);
-        GAE_STAMP(1 + k);
+        GAE_STAMP_LANDED(1 + k);
         wait_flag(&L.scanned[k], gen);
         GAE_STAMP(9 + k);
         float s32 = 0.0f, q32 = 0.0f, sft = 0.0f;
@@ -651,7 +661,7 @@ __global__ __launch_bounds__(kPChunks * kWave) void gae_aff_kernel(
         L.coef[e0 + j][r0 + row] = cf;
       }
     }
-    GAE_STAMP(1 + k);
+    GAE_STAMP_LANDED(1 + k);
     // the next iteration's operands go out now: they land while this one is scanned and stored
     if (q + 1 < niter) load(q + 1, nxt);
     // local scan of the chunk from the identity, lane = env (this wave's own LDS rows: its LDS
