@@ -1465,15 +1465,15 @@ int dppo_peer_selftest(dppo_handle* h, void* stream) {
   float* df = nullptr;
   double* dd = nullptr;
   float *slab = nullptr, *pm = nullptr, *grad = nullptr;
-  DPPO_TRY(dalloc(&df, n));
-  DPPO_TRY(dalloc(&dd, 2));
   const bool fused = h->xfused && h->radam_ok && h->ra_tags;
-  if (fused) {
-    DPPO_TRY(dalloc(&slab, h->slab_stride));
-    DPPO_TRY(dalloc(&pm, 3 * h->layout.total));
-    DPPO_TRY(dalloc(&grad, n));
-  }
   auto run = [&]() -> int {
+    DPPO_TRY(dalloc(&df, n));
+    DPPO_TRY(dalloc(&dd, 2));
+    if (fused) {
+      DPPO_TRY(dalloc(&slab, h->slab_stride));
+      DPPO_TRY(dalloc(&pm, 3 * h->layout.total));
+      DPPO_TRY(dalloc(&grad, n));
+    }
     // DPPO_PEER_SELFTEST_SKEW=r (tests): rank r contributes one wrong element to exchange 0, as
     // a rank reading stale or incoherent peer memory would see it
     const char* skew = std::getenv("DPPO_PEER_SELFTEST_SKEW");
@@ -1547,13 +1547,8 @@ int dppo_peer_selftest(dppo_handle* h, void* stream) {
   const int rc = run();
   h->xticks = ticks;
   (void)hipStreamSynchronize(s);
-  (void)hipFree(df);
-  (void)hipFree(dd);
-  if (fused) {
-    (void)hipFree(slab);
-    (void)hipFree(pm);
-    (void)hipFree(grad);
-  }
+  for (void* p : {(void*)df, (void*)dd, (void*)slab, (void*)pm, (void*)grad})
+    if (p) (void)hipFree(p);
   return rc;
 }
 

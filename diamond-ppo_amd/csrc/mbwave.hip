@@ -595,14 +595,24 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     const int k = tid + i * kThreadsW;
     const int mi = k >> 10, e = k & 1023, row = e >> 4, g = e & 15;
     const int64_t off = mi == 0 ? po.W2 : (mi == 1 ? po.Wa : po.Wc);
+#ifdef DPPO_ABL_NOSTAGE
+    // timing-only ablation (wrong results): no weight loads in the prologue -- the upper bound of
+    // what a prebuilt LDS image would save
+    wld[i] = (f32x4){(float)off, 0.f, 0.f, (float)(row + g)};
+#else
     wld[i] = *(const f32x4*)(P + off + row * H + 4 * g);
+#endif
   }
 #pragma unroll
   for (int i = 0; i < kW1Ld; ++i) {
     const int k = tid + i * kThreadsW;
     const int t = k % (4 * NIB), qq = (k / (4 * NIB)) & 3, row = k / (16 * NIB), c = 4 * t + qq;
     const bool on = k < kW1N && c < D;
+#ifdef DPPO_ABL_NOSTAGE
+    w1ld[i] = (float)(on ? row * D + c : 0);
+#else
     w1ld[i] = P[po.W1 + (on ? row * D + c : 0)];
+#endif
   }
   const float wold = P[po.Wo + ((tid >> 6) < a.A ? tid : 0)];
   const float wold2 = P[po.Wo + ((tid >> 6) + 4 < a.A ? tid + 4 * H : 0)];
