@@ -316,7 +316,8 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ val,
     const float* __restrict__ nval, float* __restrict__ adv, float* __restrict__ ret,
-    double* __restrict__ partials, int T, int N, float g, float c, int wt, int stagger) {
+    double* __restrict__ partials, int T, int N, float g, float c, int wt, int stagger,
+    int psleep) {
   __shared__ __attribute__((aligned(16))) PipeLds<E> L;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ntiles = N / E;
@@ -478,7 +479,12 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
             // behind it: flag round trip, then data round trip)
 #pragma unroll
             for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(d[set][q]), "+v"(cf[set][q]));
-          } while (f < gen);
+            if (f >= gen) break;
+            // (psleep: back off between unsuccessful polls -- each poll is 9 LDS reads, which
+            // otherwise compete with the owners' term writes for the LDS)
+            if (psleep == 1) __builtin_amdgcn_s_sleep(1);
+            else if (psleep >= 2) __builtin_amdgcn_s_sleep(2);
+          } while (true);
         };
         poll(kPChunks - 1, (kPChunks - 1) % 3);
         pf[kPChunks - 1] = gen;
@@ -982,13 +988,18 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     const bool e32 = env_e == 32 ? N % 32 == 0 : (env_e == 16 ? false : (N % 32 == 0 && N / 32 >= cus));
     // 64-env tiles (256-B rows) where they still give every CU a tile (N >= 16,384 on 256 CUs):
     // at N = 65,536 41.0 us per launch against 43.6 with 32-env tiles (exact mode, same box)
-    const bool e64 = (env_e == 64 || env_e == 0) && N % 64 == 0 && N / 64 >= cus;
+    const bool e64 = N % 64 == 0 && (env_e == 64 || (env_e == 0 && N / 64 >= cus));
     // DPPO_GAE_WT=0/1: plain or write-through (sc1) advantage / return stores (A/B timing)
     static const int wt = std::getenv("DPPO_GAE_WT") ? std::atoi(std::getenv("DPPO_GAE_WT")) : 0;
     // Cycles between the owners' first load bursts: 450-750 measured 8.0-8.25 us per launch at
     // N = 8192 against 9.1 without (1,200: 9.6, 1,800: 10.6).  DPPO_GAE_STAGGER overrides (A/B).
     static const int stagger =
         std::getenv("DPPO_GAE_STAGGER") ? std::atoi(std::getenv("DPPO_GAE_STAGGER")) : 640;
+    // The scan wave's back-off between unsuccessful polls (s_sleep 1): 7.67-7.98 against
+    // 7.90-8.19 us per launch at N = 8192 (rocprof, 3 A/B reps; s_sleep 2: 8.01-8.32).
+    // DPPO_GAE_PSLEEP=0/1/2 overrides (A/B).
+    static const int psleep =
+        std::getenv("DPPO_GAE_PSLEEP") ? std::atoi(std::getenv("DPPO_GAE_PSLEEP")) : 1;
     const int tiles = e64 ? N / 64 : (e32 ? N / 32 : G);
     int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
     if (!e32 && grid >= 16) grid -= grid % 16;
@@ -999,7 +1010,7 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
                     nv, adv, ret, partials, T, N, gamma, c, stagger);
       else
         DPPO_LAUNCH(gae_pipe_kernel<64>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                    adv, ret, partials, T, N, gamma, c, wt, stagger);
+                    adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
     } else if (mode == DPPO_GAE_AFFINE) {
       if (e32)
         DPPO_LAUNCH(gae_aff_kernel<32>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
@@ -1009,10 +1020,10 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
                     nv, adv, ret, partials, T, N, gamma, c, stagger);
     } else if (e32)
       DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c, wt, stagger);
+                  adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
     else
       DPPO_LAUNCH(gae_pipe_kernel<16>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c, wt, stagger);
+                  adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
   } else if (vec)
     DPPO_LAUNCH(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
                        partials, T, N, gamma, c);
