@@ -490,10 +490,6 @@ struct GRec {
 #ifndef DPPO_MBW_PREHEADS
 #define DPPO_MBW_PREHEADS 1
 #endif
-// Head back-propagation Wo^T dl on MFMA for 4 discrete heads (-DDPPO_MBW_MFMA_DA=0: VALU, A/B)
-#ifndef DPPO_MBW_MFMA_DA
-#define DPPO_MBW_MFMA_DA 1
-#endif
 template <int AMAX, bool CONT, int NIB>
 constexpr bool kPreloadHeads() {
   return DPPO_MBW_PREHEADS && AMAX <= 4;
@@ -1040,15 +1036,9 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     f32x4 dza[4], dzc[4];
     // 5-8 heads: Wo^T dl on MFMA (k = head, two k-steps; A = Wo[4ks + q][16 ob + r], B = the
     // delta of head 4ks + q of sample r), the N layout directly
-    // 4 discrete heads: the same product as ONE k-step per output block (4 MFMAs, A = Wo[q][16 ob
-    // + r]) instead of 64 VALU FMAs -- VALU beside fp32 MFMAs costs its issue cycles (§3.1)
-    constexpr bool kMfmaDa = AMAX == 4 && !CONT && DPPO_MBW_MFMA_DA;
-    constexpr int NKS = kMfmaHeads ? 2 : (kMfmaDa ? 1 : 0);
-    float bsel[2], woD[4];
+    float bsel[2];
 #pragma unroll
-    for (int ob = 0; ob < (kMfmaDa ? 4 : 0); ++ob) woD[ob] = lds[L.Wo + q * H + 16 * ob + r];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
+    for (int ks = 0; ks < (kMfmaHeads ? 2 : 0); ++ks)
       bsel[ks] = q == 0 ? dl[4 * ks] : (q == 1 ? dl[4 * ks + 1] : (q == 2 ? dl[4 * ks + 2] : dl[4 * ks + 3]));
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) {
@@ -1056,8 +1046,6 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       if (kMfmaHeads) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) da = mfma4(woA[ks][ob], bsel[ks], da);
-      } else if (kMfmaDa) {
-        da = mfma4(woD[ob], bsel[0], da);
       } else {
 #pragma unroll
         for (int h = 0; h < AMAX; ++h)
