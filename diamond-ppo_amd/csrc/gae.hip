@@ -450,7 +450,9 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     // The scan is the youngest wave of the workgroup and shares its SIMD with two owners: at the
     // default priority every owner VALU instruction issues first (age order) and the dependent
     // chain crawls at ~30 cycles per step.  It is the critical path: give it the SIMD.
-    __builtin_amdgcn_s_setprio(3);
+    // (psleep & 4, A/B: raise it only once the first chunk has been seen, so that the owners on
+    // this SIMD issue their first loads at normal priority)
+    if (!(psleep & 4)) __builtin_amdgcn_s_setprio(3);
     for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
       float a = 0.0f;  // advantage carried backwards, 0 after the last step (ppo.py:198)
       for (int s = 0; s < nsup; ++s) {
@@ -482,11 +484,12 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
             if (f >= gen) break;
             // (psleep: back off between unsuccessful polls -- each poll is 9 LDS reads, which
             // otherwise compete with the owners' term writes for the LDS)
-            if (psleep == 1) __builtin_amdgcn_s_sleep(1);
-            else if (psleep >= 2) __builtin_amdgcn_s_sleep(2);
+            if ((psleep & 3) == 1) __builtin_amdgcn_s_sleep(1);
+            else if ((psleep & 3) >= 2) __builtin_amdgcn_s_sleep(2);
           } while (true);
         };
         poll(kPChunks - 1, (kPChunks - 1) % 3);
+        if (psleep & 4) __builtin_amdgcn_s_setprio(3);
         pf[kPChunks - 1] = gen;
         // speculative prefetch of chunk k-1 / k-2: its flag is read before its data (LDS
         // operations of one wave complete in order), so a set flag proves the data current
