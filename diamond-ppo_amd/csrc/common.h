@@ -69,6 +69,7 @@ extern thread_local LaunchTiming g_launch_timing;
 constexpr int kWave = 64;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 

@@ -193,6 +193,103 @@ __device__ __forceinline__ void mfma4_acc(float a, float b, f32x4& c) {
   c = mfma4(a, b, c);
 }
 
+// ---- Packed fp32 (VOP3P) element-wise steps: two elements per instruction at the issue cost of
+// one scalar VALU instruction, beside the fp32 MFMAs as alone (tools/probe/mfma_kind.py: v_fma_f32
+// and v_pk_fma_f32 both 5.5 cycles per instruction beside v_mfma_f32_16x16x4_f32).  Written as
+// inline asm on the two 64-bit halves of an f32x4 (aligned register pairs, no moves): the
+// compiler's own packing (-packed-fp32-ops on) paired elements of different tiles and paid v_mov
+// and v_xor for it (C3 loop: +55 moves for 157 packed instructions).  The hazard recognizer does
+// not see inline asm, so tools/mfma_hazards.py audits these too (rules R4-R8).
+__device__ __forceinline__ f32x2 lo2(f32x4 v) { return __builtin_shufflevector(v, v, 0, 1); }
+__device__ __forceinline__ f32x2 hi2(f32x4 v) { return __builtin_shufflevector(v, v, 2, 3); }
+__device__ __forceinline__ f32x4 cat2(f32x2 a, f32x2 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3); }
+#ifdef DPPO_MBW_PK_ASM
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
+  f32x2 d;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// a * s[S] + c: element S of the pair s broadcast to both lanes
+template <int S>
+__device__ __forceinline__ f32x2 pk_fma_bc(f32x2 a, f32x2 s, f32x2 c) {
+  f32x2 d;
+  if constexpr (S == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(s), "v"(c));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(d) : "v"(a), "v"(s), "v"(c));
+  return d;
+}
+template <int S>
+__device__ __forceinline__ f32x2 pk_mul_bc(f32x2 a, f32x2 s) {
+  f32x2 d;
+  if constexpr (S == 0)
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(d) : "v"(a), "v"(s));
+  else
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(d) : "v"(a), "v"(s));
+  return d;
+}
+// e + 1 (e from v_exp: the s_nop covers the transcendental-forwarding wait state)
+__device__ __forceinline__ f32x2 pk_add1(f32x2 e) {
+  f32x2 d;
+  asm("s_nop 0\n\tv_pk_add_f32 %0, %1, 1.0 op_sel_hi:[1,0]" : "=v"(d) : "v"(e));
+  return d;
+}
+// 1 - 2 r (r from v_rcp)
+__device__ __forceinline__ f32x2 pk_one_m2(f32x2 r) {
+  f32x2 d;
+  asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, -2.0, 1.0 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(r));
+  return d;
+}
+// d (1 - y^2): the tanh derivative applied to an incoming gradient, two instructions a pair
+__device__ __forceinline__ f32x2 pk_dtanh(f32x2 dy, f32x2 y) {
+  f32x2 t;
+  asm("v_pk_fma_f32 %0, %1, %1, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(t) : "v"(y));
+  return pk_mul(dy, t);
+}
+#else
+// (the default: the same operations as compiler vector code -- this file builds with packed fp32
+// on and the SLP vectorizer off, so only these explicit f32x2 operations become packed
+// instructions, and the hazard recognizer sees them)
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) { return a * b; }
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+template <int S>
+__device__ __forceinline__ f32x2 pk_fma_bc(f32x2 a, f32x2 s, f32x2 c) {
+  return __builtin_elementwise_fma(a, __builtin_shufflevector(s, s, S, S), c);
+}
+template <int S>
+__device__ __forceinline__ f32x2 pk_mul_bc(f32x2 a, f32x2 s) {
+  return a * __builtin_shufflevector(s, s, S, S);
+}
+__device__ __forceinline__ f32x2 pk_add1(f32x2 e) { return e + 1.0f; }
+__device__ __forceinline__ f32x2 pk_one_m2(f32x2 r) {
+  return __builtin_elementwise_fma((f32x2)(-2.0f), r, (f32x2)(1.0f));
+}
+__device__ __forceinline__ f32x2 pk_dtanh(f32x2 dy, f32x2 y) {
+  return dy * __builtin_elementwise_fma(-y, y, (f32x2)(1.0f));
+}
+#endif
+__device__ __forceinline__ f32x4 dtanh4(f32x4 dy, f32x4 y) {
+  return cat2(pk_dtanh(lo2(dy), lo2(y)), pk_dtanh(hi2(dy), hi2(y)));
+}
+// sum_k w[k] x[k] over four f32x4 pairs of 16 elements: 8 packed instructions + 1 add
+__device__ __forceinline__ float pk_dot16(const f32x4 (&w)[4], const f32x4 (&x)[4]) {
+  f32x2 p = pk_mul(lo2(w[0]), lo2(x[0]));
+  p = pk_fma(hi2(w[0]), hi2(x[0]), p);
+#pragma unroll
+  for (int b = 1; b < 4; ++b) {
+    p = pk_fma(lo2(w[b]), lo2(x[b]), p);
+    p = pk_fma(hi2(w[b]), hi2(x[b]), p);
+  }
+  return p[0] + p[1];
+}
+
 __device__ __forceinline__ float tanh_w(float x) {
   // tanh = 1 - 2 / (e^{2x} + 1): five instructions (v_exp, v_rcp and three plain ones) beside a
   // wave's MFMAs; saturates to +-1 through e^{2x} = inf / 0, absolute error <= ~1.2e-7 (the
@@ -215,16 +312,17 @@ constexpr float kInvTS2 = 1.0f / (kTS * kTS);
 // Sixteen activations stage by stage (all exps, all adds, ...) from pre-scaled inputs kTS z:
 // consecutive instructions are independent, so that pinned between MFMAs each issue slot holds
 // work that is ready.
+// The two plain steps as packed instructions (two elements each, above).
 __device__ __forceinline__ void tanh4(f32x4 (&y)[4]) {
-  float e[16];
+  f32x4 e[4];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(y[i >> 2][i & 3]);
+  for (int i = 0; i < 16; ++i) e[i >> 2][i & 3] = __builtin_amdgcn_exp2f(y[i >> 2][i & 3]);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) e[i] = e[i] + 1.0f;
+  for (int i = 0; i < 4; ++i) e[i] = cat2(pk_add1(lo2(e[i])), pk_add1(hi2(e[i])));
 #pragma unroll
-  for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_rcpf(e[i]);
+  for (int i = 0; i < 16; ++i) e[i >> 2][i & 3] = __builtin_amdgcn_rcpf(e[i >> 2][i & 3]);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) y[i >> 2][i & 3] = __builtin_fmaf(-2.0f, e[i], 1.0f);
+  for (int i = 0; i < 4; ++i) y[i] = cat2(pk_one_m2(lo2(e[i])), pk_one_m2(hi2(e[i])));
 }
 
 // Sum over the four lanes of a sample (q = 0..3, same r): rows 0+1 and 2+3 with
@@ -434,6 +532,12 @@ __device__ __forceinline__ void put_n(float* sm, const f32x4 (&n)[4], int q, int
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) *(f32x4*)(sm + r * kSm + 16 * ob + 4 * q) = n[ob];
 }
+// The same reads without the renaming: x[v][b] = t[b][v] (x[v] is one loaded 16-B quad, an
+// aligned register tuple that packed instructions can take by halves).
+__device__ __forceinline__ void get_p_raw(f32x4 (&x)[4], const float* sm, int q, int r) {
+#pragma unroll
+  for (int v = 0; v < 4; ++v) x[v] = *(const f32x4*)(sm + (4 * q + v) * kSm + 4 * r);
+}
 __device__ __forceinline__ void get_p(f32x4 (&t)[4], const float* sm, int q, int r) {
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
@@ -550,14 +654,18 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
     return f;
   };
-  auto gather = [&](const Fetch& f) {
-    GRec<NIB> g;
+  // a group's layer-1 inputs (N layout) ...
+  auto gather_xn = [&](const Fetch& f, GRec<NIB>& g) {
     const float* rn = a.rec + (int64_t)f.sn * R;
 #pragma unroll
     for (int t = 0; t < 4 * NIB; ++t) {
       const int c = 4 * t + q;
       g.xn[t] = rn[c < D ? c : D - 1];
     }
+  };
+  // ... and the rest of its records
+  auto gather_rest = [&](const Fetch& f, GRec<NIB>& g) {
+    const float* rn = a.rec + (int64_t)f.sn * R;
 #pragma unroll
     for (int ib = 0; ib < NIB; ++ib)
 #pragma unroll
@@ -569,6 +677,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     g.ca[0] = CONT && !kLateCa ? *(const f32x4*)(rn + a.D8 + 4) : z4();
     g.ca[1] = (CONT && !kLateCa && AMAX > 4) ? *(const f32x4*)(rn + a.D8 + 8) : z4();
     g.sn = f.sn;
+  };
+  auto gather = [&](const Fetch& f) {
+    GRec<NIB> g;
+    gather_xn(f, g);
+    gather_rest(f, g);
     return g;
   };
 
@@ -714,9 +827,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   f32x4 gx1 = z4();  // X1: dW1[4r + b][16] partial over this lane's samples 4q + v
   // P-form partials (component b = feature 4r + b, summed over this lane's samples 4q + v)
   f32x4 gb1 = z4(), gb2 = z4(), gba = z4(), gbc = z4(), gWv = z4();
-  f32x4 gWo[kMfmaWo ? 1 : AMAX];
+  // gWo[4c + cb][i] = dWo[head 4c + i][feature 4r + cb], partial over this lane's samples
+  constexpr int kNWo = kMfmaWo ? 1 : 4 * ((AMAX + 3) / 4);
+  f32x4 gWo[kNWo];
 #pragma unroll
-  for (int h = 0; h < (kMfmaWo ? 1 : AMAX); ++h) gWo[h] = z4();
+  for (int h = 0; h < kNWo; ++h) gWo[h] = z4();
   // kMfmaWo: tile cb, lane (q, r), register i = dWo[head 4q + i][feature 4r + cb]
   f32x4 gWoT[4] = {z4(), z4(), z4(), z4()};
   float gbo[AMAX], gls[AMAX], gbv = 0.f, s_pi = 0.f, s_v = 0.f, s_ent = 0.f;
@@ -753,6 +868,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   };
   // (only where the registers allow it: the other instantiations would spill)
   constexpr bool kHoistL1 = !CONT && NIB == 1 && AMAX <= 4;
+#ifdef DPPO_MBW_LATE_XN
+  constexpr bool kEarlyXn = false;
+#else
+  constexpr bool kEarlyXn = kHoistL1;
+#endif
   f32x4 h1[4];
   if (kHoistL1 && nk > 0) layer1(h1, g_cur);
   PHASE_FENCE();
@@ -821,11 +941,13 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int h = 0; h < (kMfmaHeads ? 0 : AMAX); ++h) {
         float s = 0.f;
+        if (kPreHeads) {
+          s = pk_dot16(wo[kPreHeads ? h : 0], a1);
+        } else {
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob)
-          s += dot4(kPreHeads ? wo[kPreHeads ? h : 0][ob]
-                              : *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q),
-                    a1[ob]);
+          for (int ob = 0; ob < 4; ++ob)
+            s += dot4(*(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q), a1[ob]);
+        }
         out[h] = qsum(s) + lds[L.bo + h];
       }
       SG_DSR(4 + 4 * AMAX);
@@ -871,11 +993,17 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     put_n(sy, c1, q, r);
     PHASE_FENCE();
     WSTAMP(k, 3);
+    // the next group's layer-1 inputs, two phases before the rest of its records: its layer 1
+    // runs in this group's phase 9 (kHoistL1), and from phase 7 the records did not always land
+    // in time (a 1M-sample record buffer: ~0.8 K cycles per group waited in phase 9 at C3)
+    GRec<NIB> g_nxt{};
+    if (kEarlyXn && k + 1 < nk) gather_xn(f_nxt, g_nxt);
     // the actor / critic hidden layers in the P layout for the head weight gradients of phase 6,
     // requested now: they land during the loss chain instead of starting phase 6 with a wait
-    f32x4 a1t[4], c1t[4];
-    get_p(a1t, sx, q, r);
-    get_p(c1t, sy, q, r);
+    // (as loaded quads: a1x[v][cb] = feature 4r + cb of sample 4q + v)
+    f32x4 a1x[4], c1x[4];
+    get_p_raw(a1x, sx, q, r);
+    get_p_raw(c1x, sy, q, r);
     // Gaussian heads: the loss phase's constants (1 / (2 var), 1 / var, 1 / sigma per action; the
     // entropy and log-prob-constant sums) as ONE batch of LDS reads here -- read at their use,
     // each was an exposed LDS round trip inside the dependent loss chain (~10 per group)
@@ -896,9 +1024,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     for (int ob = 0; ob < 4; ++ob)
       wvb[ob] = kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q);
     const float kbv = lds[L.bv];
-    float vpart = 0.f;
-#pragma unroll
-    for (int ob = 0; ob < 4; ++ob) vpart += dot4(wvb[ob], c1[ob]);
+    const float vpart = pk_dot16(wvb, c1);
     const float val = qsum(vpart) + kbv;
     // ---- (5) per-sample loss and head deltas (ppo.py:264-280)
     const f32x4 sc = g_cur.sc;
@@ -1016,26 +1142,40 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
           const float dvs = kMfmaHeads ? dvv[v] : sd[kSdw * (4 * q + v) + kDv];
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb) {
-            gWoT[cb] = mfma4(dr, a1t[cb][v], gWoT[cb]);
-            gWv[cb] += dvs * c1t[cb][v];
+            gWoT[cb] = mfma4(dr, a1x[v][cb], gWoT[cb]);
+            gWv[cb] += dvs * c1x[v][cb];
           }
           continue;
         }
         f32x4 d4[NDL / 4];
 #pragma unroll
         for (int c = 0; c < NDL / 4; ++c) d4[c] = *(const f32x4*)(sd + kSdw * (4 * q + v) + 4 * c);
-        const float dvs = sd[kSdw * (4 * q + v) + kDv];
+        // the value delta with its neighbour as an aligned pair (element 0 broadcast below)
+        const f32x2 dvp = *(const f32x2*)(sd + kSdw * (4 * q + v) + kDv);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
+          // gWo[4c + cb] = dWo partials of heads 4c .. 4c + 3 for feature 4r + cb: the lane's
+          // head deltas times a1 (feature 4r + cb, sample 4q + v) broadcast, two packed FMAs
+          const f32x2 ap = (cb & 2) ? hi2(a1x[v]) : lo2(a1x[v]);
 #pragma unroll
-          for (int h = 0; h < AMAX; ++h) gWo[h][cb] += d4[h >> 2][h & 3] * a1t[cb][v];
-          gWv[cb] += dvs * c1t[cb][v];
+          for (int c = 0; c < (AMAX + 3) / 4; ++c) {
+            f32x4& g = gWo[4 * c + cb];
+            if (cb & 1)
+              g = cat2(pk_fma_bc<1>(lo2(d4[c]), ap, lo2(g)), pk_fma_bc<1>(hi2(d4[c]), ap, hi2(g)));
+            else
+              g = cat2(pk_fma_bc<0>(lo2(d4[c]), ap, lo2(g)), pk_fma_bc<0>(hi2(d4[c]), ap, hi2(g)));
+          }
         }
+        // gWv (component cb) += dv * c1 (features 4r + 0..3 of sample 4q + v)
+        gWv = cat2(pk_fma_bc<0>(lo2(c1x[v]), dvp, lo2(gWv)), pk_fma_bc<0>(hi2(c1x[v]), dvp, hi2(gWv)));
       }
     }
     f32x4 dza[4], dzc[4];
     // 5-8 heads: Wo^T dl on MFMA (k = head, two k-steps; A = Wo[4ks + q][16 ob + r], B = the
     // delta of head 4ks + q of sample r), the N layout directly
+    f32x2 dlp[(AMAX + 1) / 2];
+#pragma unroll
+    for (int c = 0; c < (AMAX + 1) / 2; ++c) dlp[c] = (f32x2){dl[2 * c], dl[2 * c + 1]};
     float bsel[2];
 #pragma unroll
     for (int ks = 0; ks < (kMfmaHeads ? 2 : 0); ++ks)
@@ -1046,17 +1186,32 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       if (kMfmaHeads) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) da = mfma4(woA[ks][ob], bsel[ks], da);
+      } else if (kPreHeads) {
+        // sum_h Wo[h] dl[h]: dl[h] broadcast from its pair, two packed FMAs per head (the same
+        // operations in the same order as the scalar chain)
+        f32x2 alo = pk_mul_bc<0>(lo2(wo[0][ob]), dlp[0]), ahi = pk_mul_bc<0>(hi2(wo[0][ob]), dlp[0]);
+#pragma unroll
+        for (int h = 1; h < AMAX; ++h) {
+          const f32x4 w = wo[kPreHeads ? h : 0][ob];
+          if (h & 1) {
+            alo = pk_fma_bc<1>(lo2(w), dlp[h >> 1], alo);
+            ahi = pk_fma_bc<1>(hi2(w), dlp[h >> 1], ahi);
+          } else {
+            alo = pk_fma_bc<0>(lo2(w), dlp[h >> 1], alo);
+            ahi = pk_fma_bc<0>(hi2(w), dlp[h >> 1], ahi);
+          }
+        }
+        da = cat2(alo, ahi);
       } else {
 #pragma unroll
         for (int h = 0; h < AMAX; ++h)
-          da += (kPreHeads ? wo[kPreHeads ? h : 0][ob]
-                           : *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q)) * dl[h];
+          da += *(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q) * dl[h];
       }
-      dza[ob] = da * (1.0f - a1[ob] * a1[ob]);
-      dzc[ob] = ((kMfmaHeads ? wvc[ob]
-                             : (kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q))) *
-                 dv) *
-                (1.0f - c1[ob] * c1[ob]);
+      dza[ob] = dtanh4(da, a1[ob]);
+      dzc[ob] = dtanh4((kMfmaHeads ? wvc[ob]
+                                   : (kPreHeads ? wv[ob] : *(const f32x4*)(lds + L.Wv + 16 * ob + 4 * q))) *
+                           dv,
+                       c1[ob]);
     }
     put_n(sx, dza, q, r);
     put_n(sy, dzc, q, r);
@@ -1085,8 +1240,10 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
     bwdP2(dh2, Wa, dza, Wc, dzc, q, r, dh2_pre);
     // the next group's records (its indices came one group ago) and the indices after that
-    GRec<NIB> g_nxt{};
-    if (k + 1 < nk) g_nxt = gather(f_nxt);
+    if (k + 1 < nk) {
+      if (!kEarlyXn) gather_xn(f_nxt, g_nxt);
+      gather_rest(f_nxt, g_nxt);
+    }
     if (k + 2 < nk) f_nxt = fetch(k + 2);
     PHASE_FENCE();
     WSTAMP(k, 6);
@@ -1099,7 +1256,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       get_p(dzct, sy, q, r);
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        dz2t[b] = dh2[b] * (1.0f - h2t[b] * h2t[b]);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dz2t[b][v] = dh2[b][v] * (1.0f - h2t[b][v] * h2t[b][v]);
         gba[b] += (dzat[b][0] + dzat[b][1]) + (dzat[b][2] + dzat[b][3]);
         gbc[b] += (dzct[b][0] + dzct[b][1]) + (dzct[b][2] + dzct[b][3]);
         gb2[b] += (dz2t[b][0] + dz2t[b][1]) + (dz2t[b][2] + dz2t[b][3]);
@@ -1133,7 +1291,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       f32x4 dz1t[4];
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        dz1t[b] = dh1[b] * (1.0f - h1t[b] * h1t[b]);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dz1t[b][v] = dh1[b][v] * (1.0f - h1t[b][v] * h1t[b][v]);
         gb1[b] += (dz1t[b][0] + dz1t[b][1]) + (dz1t[b][2] + dz1t[b][3]);
       }
       wgrad<NB1, kAgprW>(gW1, dz1t, g_cur.xt);
@@ -1237,7 +1396,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     xs[b][3] = qsum(gbc[b]);
     xs[b][4] = qsum(gWv[b]);
 #pragma unroll
-    for (int h = 0; h < AMAX; ++h) xs[b][5 + h] = kMfmaWo ? 0.f : qsum(gWo[h][b]);
+    for (int h = 0; h < AMAX; ++h) xs[b][5 + h] = kMfmaWo ? 0.f : qsum(gWo[kMfmaWo ? 0 : 4 * (h >> 2) + b][h & 3]);
   }
   float sc[2 * AMAX + 4];
 #pragma unroll

@@ -37,18 +37,27 @@ constexpr float kTS = 2.8853900817779268f;
 constexpr int kQueueCap = 256;  // queued samples a wave holds before it flushes them (>= 32)
 constexpr int kMatchRound = 4;  // next_obs / obs feature pairs compared per round of loads
 
+// LDS image (floats).  Every offset is a compile-time constant, so the weight and bias reads
+// take it as an instruction immediate from one base register; only the layer-1 image's row stride
+// S1 = D8 + 4 is a run-time value (the image sits last among the weights, sized for D8 <= 32).
+// (With run-time offsets the eval kernel held ~15 of them in SGPRs and spilled 45 SGPRs into VGPR
+// lanes: v_writelane / v_readlane + hazard s_nops inside the tile loop.)
 struct LdsLayout {
-  int W1, S1;          // W1 image [H][S1], S1 = D8 + 4 (zero-padded columns D..S1)
-  int W2, Wa, Wc;      // [H][SW]
-  int Wo;              // [A][H]  (logits or mean head)
-  int Wv;              // [H]
-  int b1, b2, ba, bc;  // [H]
-  int bo, ls;          // [32]
-  int bv;              // [4]
-  int weights_end;
-  int queue;           // [kWaves][kQueueCap] int32 (eval_kernel, next-value reuse)
-  int total;           // floats
+  static constexpr int W2 = 0, Wa = H * SW, Wc = 2 * H * SW;  // [H][SW]
+  static constexpr int Wo = 3 * H * SW;                      // [A][H]  (logits or mean head)
+  static constexpr int kWoCap = 16 * H;                      // up to 16 heads
+  static constexpr int Wv = Wo + kWoCap;                     // [H]
+  static constexpr int b1 = Wv + H, b2 = b1 + H, ba = b2 + H, bc = ba + H;  // [H]
+  static constexpr int bo = bc + H, ls = bo + 32;            // [32]
+  static constexpr int bv = ls + 32;                         // [4]
+  static constexpr int W1 = bv + 4;                          // [H][S1], zero columns D..S1
+  static constexpr int kS1Max = 36;
+  static constexpr int weights_end = W1 + H * kS1Max;
+  static constexpr int queue = weights_end;  // [kWaves][kQueueCap] int32 (eval_kernel reuse mode)
+  static constexpr int total = queue + kWaves * kQueueCap;
+  int S1;
 };
+static_assert(LdsLayout::W1 % 4 == 0 && LdsLayout::Wo % 4 == 0, "16-B aligned images");
 
 struct KArgs {
   LdsLayout L;
@@ -73,24 +82,7 @@ __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
 
 LdsLayout make_layout(const MlpShape& sh) {
   LdsLayout L{};
-  int o = 0;
   L.S1 = sh.D8 + 4;
-  L.W1 = o; o += align4(H * L.S1);
-  L.W2 = o; o += H * SW;
-  L.Wa = o; o += H * SW;
-  L.Wc = o; o += H * SW;
-  L.Wo = o; o += align4(sh.A * H);
-  L.Wv = o; o += H;
-  L.b1 = o; o += H;
-  L.b2 = o; o += H;
-  L.ba = o; o += H;
-  L.bc = o; o += H;
-  L.bo = o; o += 32;
-  L.ls = o; o += 32;
-  L.bv = o; o += 4;
-  L.weights_end = o;
-  L.queue = o; o += kWaves * kQueueCap;  // eval_kernel (reuse mode): per-wave sample queues
-  L.total = o;
   return L;
 }
 
@@ -277,11 +269,26 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
 
 
 
+// A lane's layer-1 inputs: x[4q + j] = feature 8q + 4h + j of its sample (zero past D).
 __device__ __forceinline__ f32x16 load_x0_obs(const float* o, int D, int nq1, bool valid, int h) {
   f32x16 x;
 #pragma unroll
   for (int r = 0; r < 16; ++r) x[r] = 0.0f;
-  if (valid) {
+  if ((D & 3) == 0) {
+    // rows of a multiple of 4 features (16-B aligned): four features are one 16-B load (four
+    // 4-B loads under per-feature exec masks before), no branch: the address is always valid (a
+    // block past D reads the row's last one, an invalid sample row 0) and the select drops it
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < nq1) {
+        const int f = 8 * q + 4 * h;
+        const f32x4 v = *(const f32x4*)(o + (f < D ? f : D - 4));
+        const bool on = valid && f < D;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[4 * q + j] = on ? v[j] : 0.0f;
+      }
+    }
+  } else if (valid) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q < nq1) {
@@ -385,6 +392,22 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
           // loop waited for every pair: D memory round trips per tile)
           const uint32_t* p = (const uint32_t*)(a.next_obs + ic * a.D);
           const uint32_t* o = (const uint32_t*)(a.obs + (ic + a.row) * a.D);
+          if ((a.D & 3) == 0) {
+            // 16-B rows: kMatchRound 4-feature pairs per round of loads
+            for (int f0 = 0; f0 < a.D; f0 += 4 * kMatchRound) {
+              u32x4 pv[kMatchRound], ov[kMatchRound];
+#pragma unroll
+              for (int j = 0; j < kMatchRound; ++j) {
+                const int f = f0 + 4 * j < a.D ? f0 + 4 * j : a.D - 4;
+                pv[j] = *(const u32x4*)(p + f);
+                ov[j] = *(const u32x4*)(o + f);
+              }
+#pragma unroll
+              for (int j = 0; j < kMatchRound; ++j)
+                m = m & (pv[j][0] == ov[j][0]) & (pv[j][1] == ov[j][1]) & (pv[j][2] == ov[j][2]) &
+                    (pv[j][3] == ov[j][3]);
+            }
+          } else
           for (int f0 = 0; f0 < a.D; f0 += kMatchRound) {
             uint32_t pv[kMatchRound], ov[kMatchRound];
 #pragma unroll

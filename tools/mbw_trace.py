@@ -30,6 +30,8 @@ PHASES = ["L1", "L2", "La/Lc", "heads+loss", "head dW+bwd", "dh2 (+gather)", "dz
 
 def main():
     _, T, Nn, D, A, cont, pt, ptr, _ = bench.CONFIGS[os.environ.get("PHASE_CONFIG", "cartpole4096")]
+    # PHASE_N: the same shape with another number of envs (buffer footprint A/B)
+    Nn = int(os.environ.get("PHASE_N", Nn))
     Cfg = diamond.ContinuousPPOConfig if cont else diamond.PPOConfig
     Agent = diamond.ContinuousPPO if cont else diamond.PPO
     cfg = Cfg(rollout_steps=T, num_envs=Nn, verbose=False)

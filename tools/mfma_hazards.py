@@ -14,6 +14,16 @@ included; at a join the shortest distance wins):
       (16x16x4 f32 = 8-pass XDL; gfx950 adds one state to gfx940's 11)
   R3  asm MFMA reading SrcC      -> a non-MFMA instruction writing it (WAR)  >= 11 states
 
+and, for the packed-fp32 VALU steps written as inline asm (csrc/mbwave.hip `pk_*`), which the
+recognizer does not see either:
+
+  R4  asm VALU write             -> a compiler MFMA reading it (SrcA/B/C)    >= 2 states
+  R5  transcendental VALU write  -> asm VALU reading it                      >= 2 states
+      (v_exp / v_rcp / v_log / v_sqrt / v_rsq / v_sin / v_cos; gfx940 needs 1)
+  R6  compiler MFMA write of D   -> asm VALU reading or writing those regs   >= 12 states
+  R7  compiler MFMA reading SrcC -> asm VALU writing it (WAR)                >= 11 states
+  R8  asm VALU write             -> a DPP / permlane instruction reading it  >= 2 states
+
 A state is one issued instruction (`s_nop N` = N + 1).  An MFMA's own issue counts as one.  The
 count is conservative where the listing is ambiguous (an instruction's first vector operand is
 taken as written and every operand as read).  Exit status 1 and one line per violation if any.
@@ -24,6 +34,9 @@ import re
 import sys
 
 R1, R2, R3 = 2, 12, 11
+R4, R5, R6, R7, R8 = 2, 2, 12, 11, 2
+TRANS = ("v_exp_f32", "v_rcp_f32", "v_log_f32", "v_sqrt_f32", "v_rsq_f32", "v_sin_f32",
+         "v_cos_f32", "v_rcp_iflag_f32")
 CAP = 16
 REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+)(?!\w))")
 BRANCH = re.compile(r"^s_(branch|cbranch_\w+)$")
@@ -144,8 +157,9 @@ def check(kernel, items):
         elif op not in ("s_endpgm", "s_setpc_b64") and bi + 1 < len(real):
             s.append(bi + 1)
         succ.append(s)
-    # state: reg -> distance (states since) for: valu write, asm-mfma write (+ tuple), srcC read
-    empty = ({}, {}, {})
+    # state: reg -> distance (states since) for: valu write, asm-mfma write (+ tuple), asm-mfma
+    # srcC read, asm-valu write, transcendental write, compiler-mfma write, compiler-mfma srcC read
+    empty = ({}, {}, {}, {}, {}, {}, {})
     ins_state = [None] * len(real)
     ins_state[0] = empty
     work = [0]
@@ -167,11 +181,31 @@ def check(kernel, items):
     while work:
         bi = work.pop()
         st = ins_state[bi]
-        vw, mw, cr = (dict(x) for x in st)
+        vw, mw, cr, aw, tw, cmw, ccr = (dict(x) for x in st)
         for n, it in enumerate(real[bi]):
             text, is_asm = it[1], it[2]
             op, w, r, srcc = decode(text)
             is_mfma = op.startswith("v_mfma")
+            is_avalu = is_asm and op.startswith("v_") and not is_mfma
+            if is_mfma and not is_asm:
+                for x in r:
+                    if x in aw and aw[x][0] < R4:
+                        viol.add(("R4", kernel, text, x, aw[x][0]))
+            if is_avalu:
+                for x in r:
+                    if x in tw and tw[x][0] < R5:
+                        viol.add(("R5", kernel, text, x, tw[x][0]))
+                for x in set(r) | set(w):
+                    if x in cmw and cmw[x][0] < R6:
+                        viol.add(("R6", kernel, text, x, cmw[x][0]))
+                for x in w:
+                    if x in ccr and ccr[x][0] < R7:
+                        viol.add(("R7", kernel, text, x, ccr[x][0]))
+            if ("dpp" in text or "quad_perm" in text or "row_" in text or
+                    op.startswith("v_permlane")) and not is_asm:
+                for x in r:
+                    if x in aw and aw[x][0] < R8:
+                        viol.add(("R8", kernel, text, x, aw[x][0]))
             if is_asm and is_mfma:
                 for x in r:
                     if x in vw and vw[x][0] < R1:
@@ -188,7 +222,7 @@ def check(kernel, items):
                             viol.add(("R3", kernel, text, x, cr[x][0]))
             k = states(text)
             # age everything by this instruction's states, then apply its effects
-            for d in (vw, mw, cr):
+            for d in (vw, mw, cr, aw, tw, cmw, ccr):
                 for x in list(d):
                     v = d[x]
                     nv = min(CAP, v[0] + k)
@@ -199,21 +233,37 @@ def check(kernel, items):
             if is_mfma:
                 for x in w:
                     vw.pop(x, None)
+                    aw.pop(x, None)
+                    tw.pop(x, None)
                     if is_asm:
                         mw[x] = (0, tuple(w))
+                        cmw.pop(x, None)
                     else:
                         mw.pop(x, None)
-                if is_asm:
-                    for x in srcc:
+                        cmw[x] = (0,)
+                for x in srcc:
+                    if is_asm:
                         cr[x] = (0,)
+                    else:
+                        ccr[x] = (0,)
             elif op.startswith("v_"):
                 for x in w:
                     vw[x] = (0,)
                     mw.pop(x, None)
+                    cmw.pop(x, None)
+                    if is_asm:
+                        aw[x] = (0,)
+                    else:
+                        aw.pop(x, None)
+                    if op.split("_e32")[0].split("_e64")[0] in TRANS:
+                        tw[x] = (0,)
+                    else:
+                        tw.pop(x, None)
             else:
                 for x in w:     # loads: no VALU hazard, but they end an MFMA result's life
-                    vw.pop(x, None)
-        out = (vw, mw, cr)
+                    for d in (vw, aw, tw, cmw):
+                        d.pop(x, None)
+        out = (vw, mw, cr, aw, tw, cmw, ccr)
         for sb in succ[bi]:
             new = out if ins_state[sb] is None else merge(ins_state[sb], out)
             if new != ins_state[sb]:
