@@ -146,16 +146,23 @@ __device__ __forceinline__ f32x16 bias_block(const float* b, int ob, int h) {
 // Sixteen activations stage by stage from pre-scaled inputs x = kTS z: tanh z = 1 - 2 / (2^x + 1),
 // four instructions each (v_exp, v_rcp and two plain ones; saturates through 2^x = inf / 0;
 // absolute error <= ~1.2e-7), consecutive instructions independent (mbwave.hip tanh4).
+// The two plain steps as packed instructions on the accumulator's register pairs (two elements
+// per v_pk_add_f32 / v_pk_fma_f32 at the issue cost of one scalar instruction beside the MFMAs,
+// tools/probe/mfma_kind.py).
 __device__ __forceinline__ void tanh_inplace(f32x16& x) {
-  float e[16];
+  f32x2 e[8];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_exp2f(x[r]);
+  for (int r = 0; r < 16; ++r) e[r >> 1][r & 1] = __builtin_amdgcn_exp2f(x[r]);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) e[r] = e[r] + 1.0f;
+  for (int p = 0; p < 8; ++p) e[p] = e[p] + 1.0f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) e[r] = __builtin_amdgcn_rcpf(e[r]);
+  for (int r = 0; r < 16; ++r) e[r >> 1][r & 1] = __builtin_amdgcn_rcpf(e[r >> 1][r & 1]);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) x[r] = __builtin_fmaf(-2.0f, e[r], 1.0f);
+  for (int p = 0; p < 8; ++p) {
+    const f32x2 y = __builtin_elementwise_fma((f32x2)(-2.0f), e[p], (f32x2)(1.0f));
+    x[2 * p] = y[0];
+    x[2 * p + 1] = y[1];
+  }
 }
 
 // part + part of lane ^ 32 with v_permlane32_swap (a VALU lane move, no LDS round trip); the

@@ -64,6 +64,32 @@ def test_hazard_across_loop_back_edge(tmp_path):
     assert _listing(tmp_path, body) == []
 
 
+CMFMA = "v_mfma_f32_16x16x4_f32 v[10:13], {a}, {b}, v[20:23]"
+
+
+def test_asm_valu_rules(tmp_path):
+    """Inline-asm VALU (the DPPO_MBW_PK_ASM form of the packed steps) against the compiler's own
+    MFMAs, transcendentals and lane moves, which the recognizer cannot pair with it."""
+    pk = "v_pk_mul_f32 v[2:3], v[4:5], v[6:7]"
+    # R4: asm VALU result read by a compiler MFMA
+    assert _listing(tmp_path, ["asm " + pk, CMFMA.format(a="v2", b="v8")]) == ["R4"]
+    assert _listing(tmp_path, ["asm " + pk, "s_nop 1", CMFMA.format(a="v2", b="v8")]) == []
+    # R5: a transcendental result read by asm VALU
+    assert _listing(tmp_path, ["v_exp_f32_e32 v4, v9", "asm " + pk]) == ["R5"]
+    assert _listing(tmp_path, ["v_exp_f32_e32 v4, v9", "s_nop 1", "asm " + pk]) == []
+    # R6: a compiler MFMA result read by asm VALU
+    body = [CMFMA.format(a="v30", b="v31"), "s_nop 3", "asm v_pk_mul_f32 v[2:3], v[10:11], v[6:7]"]
+    assert _listing(tmp_path, body) == ["R6"]
+    body = [CMFMA.format(a="v30", b="v31"), "s_nop 7", "s_nop 3",
+            "asm v_pk_mul_f32 v[2:3], v[10:11], v[6:7]"]
+    assert _listing(tmp_path, body) == []
+    # R7: asm VALU overwriting a compiler MFMA's SrcC while it is read
+    body = [CMFMA.format(a="v30", b="v31"), "asm v_pk_mul_f32 v[20:21], v[4:5], v[6:7]"]
+    assert _listing(tmp_path, body) == ["R7"]
+    # R8: asm VALU result read by a lane move
+    assert _listing(tmp_path, ["asm " + pk, "v_permlane16_swap_b32_e32 v2, v3"]) == ["R8"]
+
+
 def test_shipped_minibatch_kernels_pass_the_audit():
     pkg = os.path.join(ROOT, "diamond-ppo_amd")
     subprocess.run(["make", "-C", pkg, "build/mbwave.s"], check=True, capture_output=True)
