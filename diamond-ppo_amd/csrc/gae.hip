@@ -914,7 +914,16 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
        i0 += (int64_t)gridDim.x * kPackTile) {
     const int ns = (int)min((int64_t)kPackTile, a.B - i0);
     const float* o = a.obs + i0 * a.D;
-    for (int e = t; e < ns * a.D; e += kPackTile) obs_s[e] = o[e];
+    // observation rows of a multiple of 4 features: 16-B loads and 16-B LDS accesses (the 4-B
+    // per-feature form put a row stride of D floats across the lanes: 8-way LDS bank conflicts at
+    // D = 8, 64 % of the kernel's LDS cycles)
+    const bool q4 = (a.D & 3) == 0 && ((uintptr_t)a.obs & 15) == 0;
+    if (q4) {
+      const f32x4* o4 = (const f32x4*)o;
+      for (int e = t; e < ns * a.D / 4; e += kPackTile) ((f32x4*)obs_s)[e] = o4[e];
+    } else {
+      for (int e = t; e < ns * a.D; e += kPackTile) obs_s[e] = o[e];
+    }
     if (a.continuous) {
       const float* ac = (const float*)a.actions + i0 * a.A;
       for (int e = t; e < ns * a.A; e += kPackTile) act_s[e] = ac[e];
@@ -923,14 +932,20 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
     if (t < ns) {
       const int64_t i = i0 + t;
       float* r = rec_s + t * a.R;
-      for (int k = 0; k < a.D8; ++k) r[k] = k < a.D ? obs_s[t * a.D + k] : 0.0f;
+      if (q4) {
+        // the record's observation part as 16-B moves (a record row is R = 12..52 floats, 16-B
+        // aligned: lanes 48+ B apart touch distinct banks within each 8-lane group)
+        const f32x4* src = (const f32x4*)(obs_s + t * a.D);
+        for (int k = 0; k < a.D8 / 4; ++k)
+          ((f32x4*)r)[k] = 4 * k < a.D ? src[k] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      } else {
+        for (int k = 0; k < a.D8; ++k) r[k] = k < a.D ? obs_s[t * a.D + k] : 0.0f;
+      }
       float adv = a.adv[i];
       if (a.advantage_norm) adv = (adv - mean) / denom;  // ppo.py:243, fp32 as the reference
       if (a.adv_out) a.adv_out[i] = adv;
-      r[a.D8 + 0] = a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]);
-      r[a.D8 + 1] = a.logp[i];
-      r[a.D8 + 2] = adv;
-      r[a.D8 + 3] = a.ret[i];
+      *(f32x4*)(r + a.D8) = (f32x4){a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]),
+                                    a.logp[i], adv, a.ret[i]};
       if (a.continuous) {
         const int na = a.R - a.D8 - 4;
         for (int k = 0; k < na; ++k) r[a.D8 + 4 + k] = k < a.A ? act_s[t * a.A + k] : 0.0f;
