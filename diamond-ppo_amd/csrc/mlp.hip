@@ -70,6 +70,7 @@ struct KArgs {
   int64_t n;
   // shapes
   int D, D8, nq1, A, R;
+  int q4;  // obs (and next_obs) rows of a multiple of 4 floats in 16-B aligned buffers
   // next-value reuse (EvalReuse): row > 0 = the buffers are a [T][row] rollout
   int64_t row;
   uint8_t* match;
@@ -285,11 +286,13 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
 
 
 // A lane's layer-1 inputs: x[4q + j] = feature 8q + 4h + j of its sample (zero past D).
-__device__ __forceinline__ f32x16 load_x0_obs(const float* o, int D, int nq1, bool valid, int h) {
+// (q4: rows of a multiple of 4 features in 16-B aligned buffers, checked on the host)
+__device__ __forceinline__ f32x16 load_x0_obs(const float* o, int D, int nq1, bool valid, int h,
+                                              bool q4) {
   f32x16 x;
 #pragma unroll
   for (int r = 0; r < 16; ++r) x[r] = 0.0f;
-  if ((D & 3) == 0) {
+  if (q4) {
     // rows of a multiple of 4 features (16-B aligned): four features are one 16-B load (four
     // 4-B loads under per-feature exec masks before), no branch: the address is always valid (a
     // block past D reads the row's last one, an invalid sample row 0) and the select drops it
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
     const int act_d = CONT ? 0 : ((const int32_t*)a.actions)[ic];
     // ---- obs: full actor-critic forward (get_logits_and_values, ppo.py:91-96)
     f32x16 x[2], y[2];
-    x[0] = load_x0_obs(a.obs + ic * a.D, a.D, a.nq1, valid, h);
+    x[0] = load_x0_obs(a.obs + ic * a.D, a.D, a.nq1, valid, h, a.q4);
     dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);       // y = h1
     dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);                         // x = h2
     dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);                         // y = critic hidden
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
           // loop waited for every pair: D memory round trips per tile)
           const uint32_t* p = (const uint32_t*)(a.next_obs + ic * a.D);
           const uint32_t* o = (const uint32_t*)(a.obs + (ic + a.row) * a.D);
-          if ((a.D & 3) == 0) {
+          if (a.q4) {
             // 16-B rows: kMatchRound 4-feature pairs per round of loads
             for (int f0 = 0; f0 < a.D; f0 += 4 * kMatchRound) {
               u32x4 pv[kMatchRound], ov[kMatchRound];
@@ -452,7 +455,7 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       continue;
     }
     // ---- next_obs: base + critic only (get_values, ppo.py:84-89)
-    x[0] = load_x0_obs(a.next_obs + ic * a.D, a.D, a.nq1, valid, h);
+    x[0] = load_x0_obs(a.next_obs + ic * a.D, a.D, a.nq1, valid, h, a.q4);
     dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
     dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);
     dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);
@@ -501,7 +504,7 @@ __global__ __launch_bounds__(kThreads, 4) void next_eval_kernel(KArgs a) {
     const bool valid = k < (int64_t)cnt;
     const int64_t i = valid ? a.list[k] : 0;
     f32x16 x[2], y[2];
-    x[0] = load_x0_obs(a.next_obs + i * a.D, a.D, a.nq1, valid, h);
+    x[0] = load_x0_obs(a.next_obs + i * a.D, a.D, a.nq1, valid, h, a.q4);
     dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
     dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);
     dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);
@@ -555,6 +558,7 @@ struct ActArgs {
   int64_t n;
   uint32_t seed_lo, seed_hi, ctr_lo, ctr_hi;
   int D, D8, nq1, A;
+  int q4;
 };
 
 __device__ __forceinline__ void load_weights_actor(float* lds, const ActArgs& a, int tid) {
@@ -597,7 +601,7 @@ __global__ __launch_bounds__(kThreads, 4) void act_kernel(ActArgs a) {
     const bool valid = i < a.n;
     const int64_t ic = valid ? i : 0;
     f32x16 x[2], y[2];
-    x[0] = load_x0_obs(a.obs + ic * a.D, a.D, a.nq1, valid, h);
+    x[0] = load_x0_obs(a.obs + ic * a.D, a.D, a.nq1, valid, h, a.q4);
     dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);       // y = h1
     dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);                         // x = h2
     dense_tanh(y, lds + L.Wa, lds + L.ba, x, l31, h);                         // y = actor hidden
@@ -758,6 +762,7 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
   k.obs = obs;
   k.actions = actions;
   k.next_obs = next_obs;
+  k.q4 = (sh.D % 4 == 0) && ((uintptr_t)obs % 16 == 0) && (!next_obs || (uintptr_t)next_obs % 16 == 0);
   k.logp = logp;
   k.values = values;
   k.next_values = next_values;
@@ -817,6 +822,7 @@ int launch_act(const MlpShape& sh, const ParamOffsets& po, const float* params, 
   k.D8 = sh.D8;
   k.nq1 = sh.D8 / 8;
   k.A = sh.A;
+  k.q4 = (sh.D % 4 == 0) && ((uintptr_t)obs % 16 == 0);
   const size_t lds = (size_t)k.L.total * sizeof(float);
   raise_lds_limits();
   const int64_t ntiles = (n + 31) / 32;

@@ -93,3 +93,35 @@ def test_next_value_reuse_is_bit_identical(T, Nn, D, A, cont, chain_frac):
         for rep in range(3):
             assert np.array_equal(full[0][k].view(np.uint32), fast[rep][k].view(np.uint32)), \
                 (k, rep, int(np.sum(full[0][k] != fast[rep][k])))
+
+
+@pytest.mark.parametrize("D,cont", [(8, False), (4, False), (20, True)])
+def test_unaligned_observation_buffers_take_the_4b_path(D, cont):
+    """The eval and pack kernels read observation rows of a multiple of 4 features with 16-B loads
+    only from 16-B aligned buffers (checked on the host); the same rollout with obs / next_obs
+    moved to a 4-B aligned address gives the same bits through the per-feature path."""
+    T, Nn, A = 16, 48, (3 if cont else 4)
+    L = N.param_layout(N.Dims(T, Nn, D, A, int(cont), H, 4, 4, 1, 0))
+    names = P.CONTINUOUS_NAMES if cont else P.DISCRETE_NAMES
+    _, flat = random_params(L, names, D, A, cont, np.random.default_rng(D))
+    ro = _rollout(T, Nn, D, A, cont, seed=7 + D, chain_frac=0.9)
+    ref = _prepare(True, T, Nn, D, A, cont, ro, flat)
+    st = ro.as_struct()
+    keep = []
+    for f in ("obs", "next_obs"):
+        t = getattr(ro, f).reshape(-1)
+        buf = torch.empty(t.numel() + 1, device=dev())
+        buf[1:].copy_(t)
+        assert buf[1:].data_ptr() % 16 != 0
+        setattr(st, f, buf[1:].data_ptr())
+        keep.append(buf)
+    torch.cuda.synchronize()
+
+    class _Shifted:
+        def as_struct(self):
+            return st
+
+    got = _prepare(True, T, Nn, D, A, cont, _Shifted(), flat)
+    for k in ref[0]:
+        for rep in range(3):
+            assert np.array_equal(ref[0][k].view(np.uint32), got[rep][k].view(np.uint32)), (k, rep)
