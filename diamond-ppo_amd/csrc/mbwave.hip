@@ -613,6 +613,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
   static_assert(!X1 || NIB == 2, "X1 is the 17-input layout");
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #ifdef DPPO_PHASE_TRACE
+  // (timing-only build: only the instantiations tools/mbw_trace.py runs -- CartPole, LunarLander,
+  // HalfCheetah; with the stamps in, the others crash ROCm 7.2's AGPR-copy rewrite pass)
+  if constexpr (!((AMAX == 2 && !CONT && NIB == 1) || (AMAX == 4 && !CONT && NIB == 1) ||
+                  (AMAX == 6 && CONT && X1)))
+    return;
   WEDGE(0, (long long)__builtin_amdgcn_s_memtime());
   WEDGE(4, (long long)__builtin_amdgcn_s_memrealtime());
 #endif
@@ -1107,6 +1112,17 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
     PHASE_FENCE();
     WSTAMP(k, 4);
+    // kLateXt: the indices of the T-layout input, a phase before its record loads (requested in
+    // phase 7 itself, the index -> record chain held the in-order wave for a memory round trip
+    // there: 2.2 K cycles of the HalfCheetah group's dh2 phase)
+    int st[4];
+    if (kLateXt) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int j = g0 + 4 * q + v;
+        st[v] = idxp[j < mm ? j : mm - 1];
+      }
+    }
     // ---- (6) head weight gradients (P layout: feature 4r + cb, samples 4q + v), then the head
     // back-propagation dza = (Wo^T dl)(1 - a1^2), dzc = Wv dv (1 - c1^2) in the N layout
     constexpr bool kPreDh2 = !kTight;  // (it would spill 6 registers there)
@@ -1224,12 +1240,6 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     WSTAMP(k, 5);
     // ---- (7) dh2 = Wa^T dza + Wc^T dzc (P layout)
     if (kLateXt) {
-      int st[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int j = g0 + 4 * q + v;
-        st[v] = idxp[j < mm ? j : mm - 1];
-      }
 #pragma unroll
       for (int ib = 0; ib < NIB; ++ib)
 #pragma unroll
