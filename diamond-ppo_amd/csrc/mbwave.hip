@@ -195,66 +195,15 @@ __device__ __forceinline__ void mfma4_acc(float a, float b, f32x4& c) {
 
 // ---- Packed fp32 (VOP3P) element-wise steps: two elements per instruction at the issue cost of
 // one scalar VALU instruction, beside the fp32 MFMAs as alone (tools/probe/mfma_kind.py: v_fma_f32
-// and v_pk_fma_f32 both 5.5 cycles per instruction beside v_mfma_f32_16x16x4_f32).  Written as
-// inline asm on the two 64-bit halves of an f32x4 (aligned register pairs, no moves): the
-// compiler's own packing (-packed-fp32-ops on) paired elements of different tiles and paid v_mov
-// and v_xor for it (C3 loop: +55 moves for 157 packed instructions).  The hazard recognizer does
-// not see inline asm, so tools/mfma_hazards.py audits these too (rules R4-R8).
+// and v_pk_fma_f32 both ~5 cycles per instruction), on the two 64-bit halves of an f32x4 (aligned
+// register pairs, no moves).  The compiler's own packing (the SLP vectorizer) paired elements of
+// different tiles and paid a v_mov / v_xor per pair.
 __device__ __forceinline__ f32x2 lo2(f32x4 v) { return __builtin_shufflevector(v, v, 0, 1); }
 __device__ __forceinline__ f32x2 hi2(f32x4 v) { return __builtin_shufflevector(v, v, 2, 3); }
 __device__ __forceinline__ f32x4 cat2(f32x2 a, f32x2 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3); }
-#ifdef DPPO_MBW_PK_ASM
-__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
-  f32x2 d;
-  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
-  f32x2 d;
-  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-// a * s[S] + c: element S of the pair s broadcast to both lanes
-template <int S>
-__device__ __forceinline__ f32x2 pk_fma_bc(f32x2 a, f32x2 s, f32x2 c) {
-  f32x2 d;
-  if constexpr (S == 0)
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(a), "v"(s), "v"(c));
-  else
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(d) : "v"(a), "v"(s), "v"(c));
-  return d;
-}
-template <int S>
-__device__ __forceinline__ f32x2 pk_mul_bc(f32x2 a, f32x2 s) {
-  f32x2 d;
-  if constexpr (S == 0)
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0]" : "=v"(d) : "v"(a), "v"(s));
-  else
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(d) : "v"(a), "v"(s));
-  return d;
-}
-// e + 1 (e from v_exp: the s_nop covers the transcendental-forwarding wait state)
-__device__ __forceinline__ f32x2 pk_add1(f32x2 e) {
-  f32x2 d;
-  asm("s_nop 0\n\tv_pk_add_f32 %0, %1, 1.0 op_sel_hi:[1,0]" : "=v"(d) : "v"(e));
-  return d;
-}
-// 1 - 2 r (r from v_rcp)
-__device__ __forceinline__ f32x2 pk_one_m2(f32x2 r) {
-  f32x2 d;
-  asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, -2.0, 1.0 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(r));
-  return d;
-}
-// d (1 - y^2): the tanh derivative applied to an incoming gradient, two instructions a pair
-__device__ __forceinline__ f32x2 pk_dtanh(f32x2 dy, f32x2 y) {
-  f32x2 t;
-  asm("v_pk_fma_f32 %0, %1, %1, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(t) : "v"(y));
-  return pk_mul(dy, t);
-}
-#else
-// (the default: the same operations as compiler vector code -- this file builds with packed fp32
-// on and the SLP vectorizer off, so only these explicit f32x2 operations become packed
-// instructions, and the hazard recognizer sees them)
+// (compiler vector code: this file builds with packed fp32 on and the SLP vectorizer off, so only
+// these explicit f32x2 operations become packed instructions, and the hazard recognizer sees
+// them -- an inline-asm form failed the audit of tools/mfma_hazards.py, rules R4-R7)
 __device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) { return a * b; }
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
   return __builtin_elementwise_fma(a, b, c);
@@ -274,7 +223,6 @@ __device__ __forceinline__ f32x2 pk_one_m2(f32x2 r) {
 __device__ __forceinline__ f32x2 pk_dtanh(f32x2 dy, f32x2 y) {
   return dy * __builtin_elementwise_fma(-y, y, (f32x2)(1.0f));
 }
-#endif
 __device__ __forceinline__ f32x4 dtanh4(f32x4 dy, f32x4 y) {
   return cat2(pk_dtanh(lo2(dy), lo2(y)), pk_dtanh(hi2(dy), hi2(y)));
 }
