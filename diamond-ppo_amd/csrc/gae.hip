@@ -253,33 +253,6 @@ __device__ __forceinline__ void stats_fold(float s32, float q32, float sft, int 
   lsq += (double)q32 + ds * (2.0 * dsum + dn * ds);
 }
 
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double x) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double lane_f64(double x, int l) {
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
-  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
-// Wave sum in a fixed order, the result valid in every lane: DPP within each 16-lane row (xor 1,
-// xor 2, half-row mirror, row mirror: VALU data moves, no LDS round trip), then the 4 row sums
-// read from lanes 0/16/32/48.  Replaces a 6-round ds_bpermute butterfly that sat at the end of
-// the launch, after the last stores.
-__device__ __forceinline__ double wave_sum_f64(double x) {
-  x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
-  x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
-  x += dpp_f64<0x141>(x);  // row_half_mirror
-  x += dpp_f64<0x140>(x);  // row_mirror
-  return (lane_f64(x, 0) + lane_f64(x, 16)) + (lane_f64(x, 32) + lane_f64(x, 48));
-}
-
 __device__ __forceinline__ void wait_flag(int* f, int gen) {
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen)
     __builtin_amdgcn_s_sleep(1);

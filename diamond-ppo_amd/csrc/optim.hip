@@ -236,8 +236,9 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
       if (r < pl.world) t += x[r];
   }
   if (p < n) grad[p] = t;
-  double q = (p < p_total) ? (double)t * (double)t : 0.0;
-  for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+  // (wave sums by DPP row moves + 4 lane reads: the 6-step __shfl_xor butterfly on doubles was
+  // 12 LDS-crossbar round trips, ~0.3 us of the launch, here and in the norm below)
+  const double q = wave_sum_f64((p < p_total) ? (double)t * (double)t : 0.0);
   if (lane == 0)
     __hip_atomic_store(tags + blockIdx.x, tag_word(epoch, (float)q), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
 #pragma unroll
   for (int j = 0; j < kTagWordsPerLane; ++j)
     if (j * 64 + lane < nb) sq += (double)__uint_as_float((unsigned)w[j]);
-  for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+  sq = wave_sum_f64(sq);
   float norm;
   const float coef = clip_coef(sq, max_norm, &norm);
   if (p < p_total) {
