@@ -31,11 +31,15 @@ __device__ long long g_ra_edges[512][5];
 #else
 #define RA_EDGE(i)
 #endif
-constexpr int kRedWaves = 16;
+#ifndef DPPO_RA_WAVES
+#define DPPO_RA_WAVES 16
+#endif
+constexpr int kRedWaves = DPPO_RA_WAVES;  // (A/B: DPPO_RA_WAVES=8, twice the loads per wave)
+constexpr int kSlabBatch = 256 / kRedWaves;  // one batch of loads in flight per lane: G = 256
 constexpr int kRedThreads = kRedWaves * 64;
 
 // Sum of slabs[g][p] over g for this block's 64 parameters (lane = parameter): wave w takes slabs
-// w, w + 16, ... in order, 16 loads in flight; the 16 wave partials are combined by wave 0 in
+// w, w + kRedWaves, ... in order, all kSlabBatch loads in flight; the wave partials are combined by wave 0 in
 // wave order.  Returns the total in wave 0 (other waves: 0).
 __device__ __forceinline__ float slab_sum(const float* __restrict__ slabs, int G, int64_t stride,
                                           int64_t p, int64_t n, float (*part)[kRedParams]) {
@@ -44,12 +48,12 @@ __device__ __forceinline__ float slab_sum(const float* __restrict__ slabs, int G
   if (p < n) {
     const float* src = slabs + p;
     int g = wave;
-    for (; g + 15 * kRedWaves < G; g += 16 * kRedWaves) {
-      float x[16];
+    for (; g + (kSlabBatch - 1) * kRedWaves < G; g += kSlabBatch * kRedWaves) {
+      float x[kSlabBatch];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = src[(int64_t)(g + kRedWaves * k) * stride];
+      for (int k = 0; k < kSlabBatch; ++k) x[k] = src[(int64_t)(g + kRedWaves * k) * stride];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += x[k];
+      for (int k = 0; k < kSlabBatch; ++k) s += x[k];
     }
     for (; g < G; g += kRedWaves) s += src[(int64_t)g * stride];
   }
