@@ -226,15 +226,18 @@ __device__ __forceinline__ f32x2 pk_dtanh(f32x2 dy, f32x2 y) {
 __device__ __forceinline__ f32x4 dtanh4(f32x4 dy, f32x4 y) {
   return cat2(pk_dtanh(lo2(dy), lo2(y)), pk_dtanh(hi2(dy), hi2(y)));
 }
-// sum_k w[k] x[k] over four f32x4 pairs of 16 elements: 8 packed instructions + 1 add
+// sum_k w[k] x[k] over four f32x4 of 16 elements: 8 packed instructions in two independent
+// chains (low and high halves) + 2 adds.  (One chain of 8: each packed FMA waited for the one
+// before it, with a wait state between dependent packed instructions on top.)
 __device__ __forceinline__ float pk_dot16(const f32x4 (&w)[4], const f32x4 (&x)[4]) {
-  f32x2 p = pk_mul(lo2(w[0]), lo2(x[0]));
-  p = pk_fma(hi2(w[0]), hi2(x[0]), p);
+  f32x2 pa = pk_mul(lo2(w[0]), lo2(x[0]));
+  f32x2 pb = pk_mul(hi2(w[0]), hi2(x[0]));
 #pragma unroll
   for (int b = 1; b < 4; ++b) {
-    p = pk_fma(lo2(w[b]), lo2(x[b]), p);
-    p = pk_fma(hi2(w[b]), hi2(x[b]), p);
+    pa = pk_fma(lo2(w[b]), lo2(x[b]), pa);
+    pb = pk_fma(hi2(w[b]), hi2(x[b]), pb);
   }
+  const f32x2 p = pa + pb;
   return p[0] + p[1];
 }
 
@@ -896,17 +899,36 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
       tanh4(a1);
       put_n(sx, a1, q, r);
       // ---- (4) heads: logits / means and value of sample r, in every lane of the sample
+      if (kPreHeads && !kMfmaHeads) {
+        // every head's dot product at once, step by step: AMAX x 2 independent packed chains
+        // (pk_dot16's order per head), so that no step waits for its predecessor
+        f32x2 pa[kPreHeads ? AMAX : 1], pb[kPreHeads ? AMAX : 1];
 #pragma unroll
-      for (int h = 0; h < (kMfmaHeads ? 0 : AMAX); ++h) {
-        float s = 0.f;
-        if (kPreHeads) {
-          s = pk_dot16(wo[kPreHeads ? h : 0], a1);
-        } else {
+        for (int h = 0; h < (kPreHeads ? AMAX : 0); ++h) {
+          pa[h] = pk_mul(lo2(wo[h][0]), lo2(a1[0]));
+          pb[h] = pk_mul(hi2(wo[h][0]), hi2(a1[0]));
+        }
+#pragma unroll
+        for (int ob = 1; ob < 4; ++ob)
+#pragma unroll
+          for (int h = 0; h < (kPreHeads ? AMAX : 0); ++h) {
+            pa[h] = pk_fma(lo2(wo[h][ob]), lo2(a1[ob]), pa[h]);
+            pb[h] = pk_fma(hi2(wo[h][ob]), hi2(a1[ob]), pb[h]);
+          }
+#pragma unroll
+        for (int h = 0; h < (kPreHeads ? AMAX : 0); ++h) {
+          const f32x2 p = pa[h] + pb[h];
+          out[h] = qsum(p[0] + p[1]) + lds[L.bo + h];
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < (kMfmaHeads ? 0 : AMAX); ++h) {
+          float s = 0.f;
 #pragma unroll
           for (int ob = 0; ob < 4; ++ob)
             s += dot4(*(const f32x4*)(lds + L.Wo + h * H + 16 * ob + 4 * q), a1[ob]);
+          out[h] = qsum(s) + lds[L.bo + h];
         }
-        out[h] = qsum(s) + lds[L.bo + h];
       }
       SG_DSR(4 + 4 * AMAX);
 #pragma unroll

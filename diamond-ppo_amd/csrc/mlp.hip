@@ -240,8 +240,9 @@ __device__ __forceinline__ void heads(float (&out)[AMAX], const float* Wo, const
       // waited for right before its dot product)
       // (16 heads: their instantiation would spill, one read at a time there)
       const float* wp = Wo + a * H + 4 * h;
-      // packed pair products (two elements per v_pk_fma_f32) summed once at the end
-      f32x2 pp = (f32x2)(0.0f);
+      // packed pair products (two elements per v_pk_fma_f32) in two independent chains, summed
+      // once at the end
+      f32x2 pa = (f32x2)(0.0f), pb = (f32x2)(0.0f);
 #pragma unroll
       for (int fb = 0; fb < 2; ++fb) {
         f32x4 w[4];
@@ -251,12 +252,13 @@ __device__ __forceinline__ void heads(float (&out)[AMAX], const float* Wo, const
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const f32x4 wq = AMAX <= 8 ? w[q] : *(const f32x4*)(wp + fb * 32 + 8 * q);
-          pp = __builtin_elementwise_fma((f32x2){wq[0], wq[1]},
-                                         (f32x2){x[fb][4 * q + 0], x[fb][4 * q + 1]}, pp);
-          pp = __builtin_elementwise_fma((f32x2){wq[2], wq[3]},
-                                         (f32x2){x[fb][4 * q + 2], x[fb][4 * q + 3]}, pp);
+          pa = __builtin_elementwise_fma((f32x2){wq[0], wq[1]},
+                                         (f32x2){x[fb][4 * q + 0], x[fb][4 * q + 1]}, pa);
+          pb = __builtin_elementwise_fma((f32x2){wq[2], wq[3]},
+                                         (f32x2){x[fb][4 * q + 2], x[fb][4 * q + 3]}, pb);
         }
       }
+      const f32x2 pp = pa + pb;
       part = pp[0] + pp[1];
     }
     out[a] = half_sum(part) + bo[a];
@@ -266,7 +268,7 @@ __device__ __forceinline__ void heads(float (&out)[AMAX], const float* Wo, const
 __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32x16 (&x)[2],
                                             int h) {
   const float* wp = Wv + 4 * h;
-  f32x2 pp = (f32x2)(0.0f);
+  f32x2 pa = (f32x2)(0.0f), pb = (f32x2)(0.0f);
 #pragma unroll
   for (int fb = 0; fb < 2; ++fb) {
     f32x4 w[4];  // a block's four slices read together (heads above)
@@ -274,12 +276,13 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
     for (int q = 0; q < 4; ++q) w[q] = *(const f32x4*)(wp + fb * 32 + 8 * q);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      pp = __builtin_elementwise_fma((f32x2){w[q][0], w[q][1]},
-                                     (f32x2){x[fb][4 * q + 0], x[fb][4 * q + 1]}, pp);
-      pp = __builtin_elementwise_fma((f32x2){w[q][2], w[q][3]},
-                                     (f32x2){x[fb][4 * q + 2], x[fb][4 * q + 3]}, pp);
+      pa = __builtin_elementwise_fma((f32x2){w[q][0], w[q][1]},
+                                     (f32x2){x[fb][4 * q + 0], x[fb][4 * q + 1]}, pa);
+      pb = __builtin_elementwise_fma((f32x2){w[q][2], w[q][3]},
+                                     (f32x2){x[fb][4 * q + 2], x[fb][4 * q + 3]}, pb);
     }
   }
+  const f32x2 pp = pa + pb;
   return half_sum(pp[0] + pp[1]) + bv;
 }
 
