@@ -292,9 +292,9 @@ __device__ __forceinline__ float value_head(const float* Wv, float bv, const f32
 // (q4: rows of a multiple of 4 features in 16-B aligned buffers, checked on the host)
 __device__ __forceinline__ f32x16 load_x0_obs(const float* o, int D, int nq1, bool valid, int h,
                                               bool q4) {
+  // (entries of k-groups q >= nq1 stay unset: dense1_tanh reads only q < nq1 -- zeroing all 16
+  // was 16 v_mov per call; an invalid sample's column is never stored)
   f32x16 x;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) x[r] = 0.0f;
   if (q4) {
     // rows of a multiple of 4 features (16-B aligned): four features are one 16-B load (four
     // 4-B loads under per-feature exec masks before), no branch: the address is always valid (a
@@ -309,14 +309,14 @@ __device__ __forceinline__ f32x16 load_x0_obs(const float* o, int D, int nq1, bo
         for (int j = 0; j < 4; ++j) x[4 * q + j] = on ? v[j] : 0.0f;
       }
     }
-  } else if (valid) {
+  } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q < nq1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int f = 8 * q + 4 * h + j;
-          x[4 * q + j] = f < D ? o[f] : 0.0f;
+          x[4 * q + j] = (valid && f < D) ? o[f] : 0.0f;
         }
       }
     }
