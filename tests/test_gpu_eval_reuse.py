@@ -79,6 +79,8 @@ def _prepare(reuse, T, Nn, D, A, cont, ro, flat):
     (8, 33, 17, 6, True, 0.8),       # Gaussian head, 17 inputs, ragged env count
     (128, 256, 4, 2, False, 0.97),   # a longer rollout with a realistic reset rate
     (2, 5, 3, 3, False, 1.0),        # minimal T for reuse
+    (8, 40, 6, 12, False, 0.5),      # 9-16 actions: the 16-head eval build
+    (8, 33, 5, 10, True, 0.8),
     (1, 16, 4, 2, False, 1.0),       # T = 1: no next row, the full evaluation
 ])
 def test_next_value_reuse_is_bit_identical(T, Nn, D, A, cont, chain_frac):

@@ -49,7 +49,9 @@ def _shapes():
 # HalfCheetah's X1 layout), each with a partial last 16-sample group.
 _HEAD_SHAPES = [(4, 2, False), (3, 1, True), (8, 3, False), (8, 4, False), (11, 4, True),
                 (20, 3, False), (16, 5, False), (8, 7, False), (16, 8, False), (17, 5, True),
-                (17, 6, True)]
+                (17, 6, True),
+                # 9-16 actions (the C-ABI's limit is 16): the two-team kernel's 16-head build
+                (6, 12, False), (5, 10, True), (32, 16, False)]
 
 
 @pytest.mark.parametrize("j,D,A,cont", [(j, *s) for j, s in enumerate(_HEAD_SHAPES)])
