@@ -196,6 +196,14 @@ def test_learn_intermediate_depth_vs_oracle(T, Nn, D, A, cont, want_depth):
     assert production_depth(mb, D, A, cont) == want_depth
 
 
+@pytest.mark.parametrize("cont", [False, True])
+def test_learn_at_the_shape_limits_vs_oracle(cont):
+    """The C-ABI's largest MLP shape, 32 inputs and 16 actions (the two-team kernel's 16-head
+    build, the 16-head eval and the widest sample records): the 32-step learn() against the
+    oracle's."""
+    learn_vs_oracle(16, 256, 32, 16, cont, seed=16 + cont)
+
+
 def test_learn_full_c2_vs_oracle():
     """BASELINE configs[1] itself: CartPole PPO, T = 128, N = 4096 (mb 65,536: four groups per
     wave of the sample-split kernel)."""
