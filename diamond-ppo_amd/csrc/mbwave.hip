@@ -895,6 +895,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     }
     SG_FENCE();
     {
+      // (reading the critic's first weight block and biases ahead of the head rows, fenced,
+      // measured slower at C3: 96.97-97.38 vs 96.24-96.52 us, tools/gpu/r04_w0c.sh)
       fwd64_raw(c1, Wc, h2, q, r);
       tanh4(a1);
       put_n(sx, a1, q, r);
