@@ -846,12 +846,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
     // DPPO_EVAL_REUSE=0: the full next_obs critic pass (A/B runs)
     const char* e = std::getenv("DPPO_EVAL_REUSE");
     h->reuse_on = dims->rollout_steps >= 2 && !(e && e[0] == '0');
-    if (h->reuse_on) {
-      chk(dalloc(&h->reuse.match, h->B));
-      chk(dalloc(&h->reuse.list, h->B));
-      chk(dalloc(&h->reuse.list_ctr, 2));
-      h->reuse.row = dims->num_envs;
-    }
+    if (h->reuse_on) h->reuse.row = dims->num_envs;
   }
   for (int k = 0; k < 2; ++k) {
     chk(dalloc(&h->perms_dev2[k], E * h->pe));
@@ -905,7 +900,6 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
     (void)hipMemset(h->dsum, 0, 4 * sizeof(double));
     (void)hipMemset(h->arrivals, 0, 4 * kArrivalWords * sizeof(unsigned));
     (void)hipMemset(h->ra_tags, 0, reduce_adam_tag_words(h->layout.total) * sizeof(uint64_t));
-    if (h->reuse_on) (void)hipMemset(h->reuse.list_ctr, 0, 2 * sizeof(unsigned));
     // the fused kernel never writes the layout's padding floats: keep them zero in every slab
     (void)hipMemset(h->slabs, 0, (size_t)h->G * h->slab_stride * sizeof(float));
   }
@@ -948,9 +942,6 @@ void dppo_destroy(dppo_handle* h) {
   (void)hipFree(h->partials);
   (void)hipFree(h->dsum);
   (void)hipFree(h->sq_part);
-  (void)hipFree(h->reuse.match);
-  (void)hipFree(h->reuse.list);
-  (void)hipFree(h->reuse.list_ctr);
   (void)hipFree(h->arrivals);
   (void)hipFree(h->ra_tags);
   for (int k = 0; k < 2; ++k) {

@@ -212,14 +212,10 @@ struct MlpShape {
 size_t mlp_lds_bytes_eval(const MlpShape& sh);
 // Next-value reuse of the old-policy evaluation over a [T][row] rollout: where next_obs[i] is
 // bitwise obs[i + row], V(next_obs[i]) = values[i + row]; only the other samples get a critic
-// pass of their own (compacted into `list` through the ping-pong counter list_ctr[par]; both
-// counters zero before the first launch).  Results are bit-identical to the full evaluation.
+// pass of their own, run by the eval kernel's waves from a wave-private LDS ring (no second
+// launch).  Results are bit-identical to the full evaluation.
 struct EvalReuse {
-  int64_t row;
-  uint8_t* match;      // [n]
-  int32_t* list;       // [n]
-  unsigned* list_ctr;  // [2]
-  int par;             // flipped by every launch
+  int64_t row;  // > 0: the buffers are a [T][row] rollout, next_obs[i] may be obs[i + row]
 };
 int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params, const float* obs,
                 const void* actions, const float* next_obs, float* logp, float* values,

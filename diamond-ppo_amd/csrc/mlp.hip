@@ -34,7 +34,7 @@ constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 // MFMAs then produce kTS z and tanh_inplace skips its multiply (one VALU instruction fewer per
 // activation; VALU is not hidden behind fp32 MFMAs on gfx950).
 constexpr float kTS = 2.8853900817779268f;
-constexpr int kQueueCap = 256;  // queued samples a wave holds before it flushes them (>= 32)
+constexpr int kQueueCap = 256;  // a wave's ring of queued critic-pass samples (power of 2, >= 96)
 constexpr int kMatchRound = 4;  // next_obs / obs feature pairs compared per round of loads
 
 // LDS image (floats).  Every offset is a compile-time constant, so the weight and bias reads
@@ -53,7 +53,7 @@ struct LdsLayout {
   static constexpr int W1 = bv + 4;                          // [H][S1], zero columns D..S1
   static constexpr int kS1Max = 36;
   static constexpr int weights_end = W1 + H * kS1Max;
-  static constexpr int queue = weights_end;  // [kWaves][kQueueCap] int32 (eval_kernel reuse mode)
+  static constexpr int queue = weights_end;  // [kWaves][kQueueCap] int32 (eval_kernel reuse ring)
   static constexpr int total = queue + kWaves * kQueueCap;
   int S1;
 };
@@ -73,10 +73,6 @@ struct KArgs {
   int q4;  // obs (and next_obs) rows of a multiple of 4 floats in 16-B aligned buffers
   // next-value reuse (EvalReuse): row > 0 = the buffers are a [T][row] rollout
   int64_t row;
-  uint8_t* match;
-  int32_t* list;
-  unsigned* list_ctr;
-  int par;
 };
 
 __host__ __device__ inline int align4(int x) { return (x + 3) & ~3; }
@@ -336,20 +332,29 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
   const LdsLayout& L = a.L;
   const float bv = lds_[L.bv];
   const int64_t ntiles = (a.n + 31) / 32;
-  // Reuse mode: the samples whose next value needs the critic pass are queued in a wave-private
-  // LDS list and appended to the global list a queue at a time -- one returning atomic per flush
-  // instead of one per tile, each of which held the wave for a device-scope round trip.
-  // (queue offset and fill count kept wave-uniform -- scalar registers: the vector ones are all
-  // taken at four waves per SIMD)
+  // Reuse mode (a.row > 0, the buffers are a [T][row] rollout): the samples whose next value
+  // needs a critic pass on next_obs are queued in a wave-private LDS ring, and the wave runs that
+  // pass itself, 32 queued samples at a time (and the remainder at the end) -- no global list, no
+  // second kernel, no copy pass.  (Queue head / fill kept wave-uniform -- scalar registers: the
+  // vector ones are all taken at four waves per SIMD.)
   const int qbase = L.queue + __builtin_amdgcn_readfirstlane(wave) * kQueueCap;
-  int qn = 0;
-  auto flush = [&]() {
-    if (qn == 0) return;
-    unsigned base = 0;
-    if (lane == 0) base = atomicAdd(a.list_ctr + a.par, (unsigned)qn);
-    base = __shfl(base, 0);
-    for (int k = lane; k < qn; k += kWave) a.list[base + k] = ((const int32_t*)lds_)[qbase + k];
-    qn = 0;
+  int qh = 0, qn = 0;
+  // critic pass (get_values, ppo.py:84-89) on next_obs of the first `cnt` queued samples: the
+  // same instructions as the obs pass's critic, so a sample's next value has the same bits
+  // whichever tile computes it
+  auto critic_queue = [&](int cnt) {
+    float* lds = opaque_base(lds_);
+    const bool qv = l31 < cnt;
+    const int64_t k = qv ? ((const int32_t*)lds_)[qbase + ((qh + l31) & (kQueueCap - 1))] : 0;
+    f32x16 x[2], y[2];
+    x[0] = load_x0_obs(a.next_obs + k * a.D, a.D, a.nq1, qv, h, a.q4);
+    dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
+    dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);
+    dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);
+    const float nv = value_head(lds + L.Wv, bv, y, h);
+    if (qv && h == 0) a.next_values[k] = nv;
+    qh = (qh + cnt) & (kQueueCap - 1);
+    qn -= cnt;
   };
   for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles;
        tile += (int64_t)gridDim.x * kWaves) {
@@ -401,18 +406,21 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       logp = za - (mx + logf(se));
     }
     if (a.row > 0) {
-      // next_obs[i] bitwise equal to obs[i + row] (the reference's rollout stores the same array
-      // for both unless the env was reset, ppo.py:163-179): V(next_obs[i]) is values[i + row],
-      // computed by this kernel's obs pass with the same instructions -- the same bits.  The
-      // other samples are queued for next_eval_kernel's critic pass.
-      bool need = false;
+      // next_obs[i - row] bitwise equal to this sample's obs[i] (the reference's rollout stores
+      // the same array for both unless the env was reset, ppo.py:163-179): V(next_obs[i - row]) is
+      // this tile's v, computed by the same instructions on the same bits -- written here.  The
+      // other predecessors, and the samples of the last row (no successor), are queued for the
+      // wave's critic pass.
+      const int64_t ip = i - a.row;
+      bool need_p = false, need_s = false;
       if (valid && h == 0) {
-        bool m = i + a.row < a.n;
-        if (m) {
+        need_s = i + a.row >= a.n;
+        if (ip >= 0) {
+          bool m = true;
           // kMatchRound features per round, all their loads in flight together (a short-circuit
           // loop waited for every pair: D memory round trips per tile)
-          const uint32_t* p = (const uint32_t*)(a.next_obs + ic * a.D);
-          const uint32_t* o = (const uint32_t*)(a.obs + (ic + a.row) * a.D);
+          const uint32_t* p = (const uint32_t*)(a.next_obs + ip * a.D);
+          const uint32_t* o = (const uint32_t*)(a.obs + ic * a.D);
           if (a.q4) {
             // 16-B rows: kMatchRound 4-feature pairs per round of loads
             for (int f0 = 0; f0 < a.D; f0 += 4 * kMatchRound) {
@@ -428,33 +436,34 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
                 m = m & (pv[j][0] == ov[j][0]) & (pv[j][1] == ov[j][1]) & (pv[j][2] == ov[j][2]) &
                     (pv[j][3] == ov[j][3]);
             }
-          } else
-          for (int f0 = 0; f0 < a.D; f0 += kMatchRound) {
-            uint32_t pv[kMatchRound], ov[kMatchRound];
+          } else {
+            for (int f0 = 0; f0 < a.D; f0 += kMatchRound) {
+              uint32_t pv[kMatchRound], ov[kMatchRound];
 #pragma unroll
-            for (int j = 0; j < kMatchRound; ++j) {
-              const int f = f0 + j < a.D ? f0 + j : a.D - 1;
-              pv[j] = p[f];
-              ov[j] = o[f];
+              for (int j = 0; j < kMatchRound; ++j) {
+                const int f = f0 + j < a.D ? f0 + j : a.D - 1;
+                pv[j] = p[f];
+                ov[j] = o[f];
+              }
+#pragma unroll
+              for (int j = 0; j < kMatchRound; ++j) m = m & (pv[j] == ov[j]);
             }
-#pragma unroll
-            for (int j = 0; j < kMatchRound; ++j) m = m & (pv[j] == ov[j]);
           }
+          if (m) a.next_values[ip] = v;
+          need_p = !m;
         }
-        a.match[i] = m ? 1 : 0;
-        need = !m;
-      }
-      const uint64_t bal = __ballot(need);
-      if (bal != 0) {
-        const int cnt = __builtin_amdgcn_readfirstlane(__popcll(bal));
-        if (qn + cnt > kQueueCap) flush();
-        if (need) ((int32_t*)lds_)[qbase + qn + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)i;
-        qn = __builtin_amdgcn_readfirstlane(qn + cnt);
-      }
-      if (valid && h == 0) {
         a.logp[i] = logp;
         a.values[i] = v;
       }
+      // enqueue (ring of kQueueCap; at most 64 per tile onto < 32 left, so it never overflows)
+      const uint64_t bp = __ballot(need_p), bs = __ballot(need_s);
+      const uint64_t below = (1ull << lane) - 1ull;
+      int32_t* qr = (int32_t*)lds_ + qbase;
+      if (need_p) qr[(qh + qn + __popcll(bp & below)) & (kQueueCap - 1)] = (int32_t)ip;
+      const int np = __builtin_amdgcn_readfirstlane(__popcll(bp));
+      if (need_s) qr[(qh + qn + np + __popcll(bs & below)) & (kQueueCap - 1)] = (int32_t)i;
+      qn = __builtin_amdgcn_readfirstlane(qn + np + __popcll(bs));
+      while (qn >= 32) critic_queue(32);
       continue;
     }
     // ---- next_obs: base + critic only (get_values, ppo.py:84-89)
@@ -469,52 +478,7 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       a.next_values[i] = nv;
     }
   }
-  flush();
-}
-
-// The critic pass on next_obs for the samples eval_kernel queued (reuse mode), and the reused
-// next values of the others: next_values[i] = values[i + row] where match[i].  Zeroes the other
-// list counter for the next eval launch (which appends to it; the last reader of that counter was
-// the previous launch of this kernel).
-__global__ __launch_bounds__(kThreads, 4) void next_eval_kernel(KArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds_[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  // the reused values (a streaming copy) after this workgroup's critic tiles (a latency-bound
-  // chain of dependent layers): the workgroups without a tile copy at once, the others overlap
-  // their tiles with them
-  auto copy_reused = [&]() {
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + tid; i < a.n;
-         i += (int64_t)gridDim.x * kThreads)
-      if (a.match[i]) a.next_values[i] = a.values[i + a.row];
-  };
-  const unsigned cnt = __hip_atomic_load(a.list_ctr + a.par, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x == 0 && tid == 0) a.list_ctr[a.par ^ 1] = 0u;
-  const int64_t ntiles = ((int64_t)cnt + 31) / 32;
-  if ((int64_t)blockIdx.x * kWaves >= ntiles) {  // no tile for this workgroup
-    copy_reused();
-    return;
-  }
-  load_weights(lds_, a, tid);
-  __syncthreads();
-  const LdsLayout& L = a.L;
-  const float bv = lds_[L.bv];
-  for (int64_t tile = (int64_t)blockIdx.x * kWaves + wave; tile < ntiles;
-       tile += (int64_t)gridDim.x * kWaves) {
-    float* lds = opaque_base(lds_);
-    const int64_t k = tile * 32 + l31;
-    const bool valid = k < (int64_t)cnt;
-    const int64_t i = valid ? a.list[k] : 0;
-    f32x16 x[2], y[2];
-    x[0] = load_x0_obs(a.next_obs + i * a.D, a.D, a.nq1, valid, h, a.q4);
-    dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
-    dense_tanh(x, lds + L.W2, lds + L.b2, y, l31, h);
-    dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);
-    const float nv = value_head(lds + L.Wv, bv, y, h);
-    if (valid && h == 0) a.next_values[i] = nv;
-  }
-  copy_reused();
+  if (qn > 0) critic_queue(qn);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -720,7 +684,6 @@ void raise_lds_limits() {
     DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
     DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
 #undef DPPO_SET
-    raise_dyn_lds((const void*)next_eval_kernel);
 #define DPPO_SET(A, C) raise_dyn_lds((const void*)act_kernel<A, C>);
     DPPO_SET(2, false) DPPO_SET(2, true) DPPO_SET(4, false) DPPO_SET(4, true)
     DPPO_SET(8, false) DPPO_SET(8, true) DPPO_SET(16, false) DPPO_SET(16, true)
@@ -754,14 +717,7 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
                 float* next_values, int64_t n, hipStream_t s, EvalReuse* reuse) {
   if (n <= 0) return DPPO_OK;
   KArgs k = base_args(sh, po, params);
-  if (reuse && reuse->row > 0 && reuse->row < n) {
-    k.row = reuse->row;
-    k.match = reuse->match;
-    k.list = reuse->list;
-    k.list_ctr = reuse->list_ctr;
-    k.par = reuse->par;
-    reuse->par ^= 1;
-  }
+  if (reuse && reuse->row > 0 && reuse->row < n) k.row = reuse->row;
   k.obs = obs;
   k.actions = actions;
   k.next_obs = next_obs;
@@ -786,10 +742,6 @@ int launch_eval(const MlpShape& sh, const ParamOffsets& po, const float* params,
   if (g > 2 * cus) g = 2 * cus;
   DPPO_DISPATCH(eval_kernel, sh, dim3((unsigned)g), lds, s, k);
   DPPO_LAUNCH_CHECK();
-  if (k.row > 0) {
-    DPPO_LAUNCH(next_eval_kernel, dim3((unsigned)g), dim3(kThreads), lds, s, k);
-    DPPO_LAUNCH_CHECK();
-  }
   return DPPO_OK;
 }
 

@@ -1,4 +1,4 @@
-"""The old-policy evaluation's next-value reuse (csrc/mlp.hip eval_kernel / next_eval_kernel).
+"""The old-policy evaluation's next-value reuse (csrc/mlp.hip eval_kernel: reused next values plus the wave-run critic pass).
 
 The reference evaluates the critic on every next_obs (ppo.py:235-238), but its rollout stores the
 array env.step returned as next_obs[t] and -- unless that env was reset -- feeds the same array in
