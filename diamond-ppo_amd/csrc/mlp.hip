@@ -54,7 +54,7 @@ struct LdsLayout {
   static constexpr int kS1Max = 36;
   static constexpr int weights_end = W1 + H * kS1Max;
   static constexpr int queue = weights_end;  // [kWaves][kQueueCap] int32 (eval_kernel reuse ring)
-  static constexpr int total = queue + kWaves * kQueueCap;
+  static constexpr int total = queue + kWaves * kQueueCap + 2 * kWaves;  // + ring counts / heads
   int S1;
 };
 static_assert(LdsLayout::W1 % 4 == 0 && LdsLayout::Wo % 4 == 0, "16-B aligned images");
@@ -342,10 +342,9 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
   // critic pass (get_values, ppo.py:84-89) on next_obs of the first `cnt` queued samples: the
   // same instructions as the obs pass's critic, so a sample's next value has the same bits
   // whichever tile computes it
-  auto critic_queue = [&](int cnt) {
+  // critic pass on sample k of each lane (qv: the lane has one)
+  auto critic_tile = [&](bool qv, int64_t k) {
     float* lds = opaque_base(lds_);
-    const bool qv = l31 < cnt;
-    const int64_t k = qv ? ((const int32_t*)lds_)[qbase + ((qh + l31) & (kQueueCap - 1))] : 0;
     f32x16 x[2], y[2];
     x[0] = load_x0_obs(a.next_obs + k * a.D, a.D, a.nq1, qv, h, a.q4);
     dense1_tanh(y, lds + L.W1, L.S1, lds + L.b1, x[0], a.nq1, l31, h);
@@ -353,6 +352,11 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
     dense_tanh(y, lds + L.Wc, lds + L.bc, x, l31, h);
     const float nv = value_head(lds + L.Wv, bv, y, h);
     if (qv && h == 0) a.next_values[k] = nv;
+  };
+  auto critic_queue = [&](int cnt) {
+    const bool qv = l31 < cnt;
+    const int64_t k = qv ? ((const int32_t*)lds_)[qbase + ((qh + l31) & (kQueueCap - 1))] : 0;
+    critic_tile(qv, k);
     qh = (qh + cnt) & (kQueueCap - 1);
     qn -= cnt;
   };
@@ -478,7 +482,36 @@ __global__ __launch_bounds__(kThreads, 4) void eval_kernel(KArgs a) {
       a.next_values[i] = nv;
     }
   }
-  if (qn > 0) critic_queue(qn);
+  if (a.row > 0) {
+    // the waves' remainders (< 32 each) pooled across the workgroup and run as full tiles: one
+    // partial critic tile per wave at the end was ~8 % more MFMA work than the queued samples need
+    int* rem = (int*)lds_ + L.queue + kWaves * kQueueCap;  // [kWaves] counts, [kWaves] heads
+    if (lane == 0) {
+      rem[wave] = qn;
+      rem[kWaves + wave] = qh;
+    }
+    __syncthreads();
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tot += rem[w];
+    if (32 * wave < tot) {
+      const int pos = 32 * wave + l31;
+      bool qv = pos < tot;
+      int64_t k = 0;
+      if (qv) {
+        int base = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+          const int c = rem[w];
+          if (pos >= base && pos < base + c)
+            k = ((const int32_t*)lds_)[L.queue + w * kQueueCap +
+                                       ((rem[kWaves + w] + pos - base) & (kQueueCap - 1))];
+          base += c;
+        }
+      }
+      critic_tile(qv, k);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -3,7 +3,7 @@
 # bit-identity tests and the rest of the parity suite touching eval, then bench A/B against
 # build/libdppo_pre.so on C3 / C2 / C4 / C5.
 set -o pipefail
-O=gpurun_out/fuse; mkdir -p $O
+O=gpurun_out/fuse2; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/test_gpu_eval_reuse.py tests/test_gpu_parity.py tests/test_gpu_production.py tests/test_gpu_rollout_ckpt.py tests/test_gpu_dataparallel.py -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/pytest.log | head -20; exit $rc; }
 lib() { [ "$1" = main ] && echo diamond-ppo_amd/diamond/libdppo.so || echo diamond-ppo_amd/build/libdppo_$1.so; }
