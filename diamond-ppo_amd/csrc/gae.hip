@@ -894,12 +894,24 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
     if (q4) {
       const f32x4* o4 = (const f32x4*)o;
       for (int e = t; e < ns * a.D / 4; e += kPackTile) ((f32x4*)obs_s)[e] = o4[e];
+    } else if (((uintptr_t)a.obs & 15) == 0) {
+      // other widths: the tile's block of ns * D floats starts 16-B aligned (i0 is a multiple of
+      // 256), so it still moves as 16-B pieces plus a scalar tail
+      const int n4 = ns * a.D / 4;
+      for (int e = t; e < n4; e += kPackTile) ((f32x4*)obs_s)[e] = ((const f32x4*)o)[e];
+      for (int e = 4 * n4 + t; e < ns * a.D; e += kPackTile) obs_s[e] = o[e];
     } else {
       for (int e = t; e < ns * a.D; e += kPackTile) obs_s[e] = o[e];
     }
     if (a.continuous) {
       const float* ac = (const float*)a.actions + i0 * a.A;
-      for (int e = t; e < ns * a.A; e += kPackTile) act_s[e] = ac[e];
+      if (((uintptr_t)a.actions & 15) == 0) {
+        const int n4 = ns * a.A / 4;
+        for (int e = t; e < n4; e += kPackTile) ((f32x4*)act_s)[e] = ((const f32x4*)ac)[e];
+        for (int e = 4 * n4 + t; e < ns * a.A; e += kPackTile) act_s[e] = ac[e];
+      } else {
+        for (int e = t; e < ns * a.A; e += kPackTile) act_s[e] = ac[e];
+      }
     }
     __syncthreads();
     if (t < ns) {
@@ -912,7 +924,12 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
         for (int k = 0; k < a.D8 / 4; ++k)
           ((f32x4*)r)[k] = 4 * k < a.D ? src[k] : (f32x4){0.f, 0.f, 0.f, 0.f};
       } else {
-        for (int k = 0; k < a.D8; ++k) r[k] = k < a.D ? obs_s[t * a.D + k] : 0.0f;
+        // (rows of other widths: four 4-B reads -- conflict-free for odd D -- then one 16-B
+        // write per quad of the record; per-float writes at the record stride conflicted)
+        const float* src = obs_s + t * a.D;
+        for (int k = 0; k < a.D8; k += 4)
+          *(f32x4*)(r + k) = (f32x4){k < a.D ? src[k] : 0.f, k + 1 < a.D ? src[k + 1] : 0.f,
+                                     k + 2 < a.D ? src[k + 2] : 0.f, k + 3 < a.D ? src[k + 3] : 0.f};
       }
       float adv = a.adv[i];
       if (a.advantage_norm) adv = (adv - mean) / denom;  // ppo.py:243, fp32 as the reference
@@ -920,8 +937,11 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
       *(f32x4*)(r + a.D8) = (f32x4){a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]),
                                     a.logp[i], adv, a.ret[i]};
       if (a.continuous) {
-        const int na = a.R - a.D8 - 4;
-        for (int k = 0; k < na; ++k) r[a.D8 + 4 + k] = k < a.A ? act_s[t * a.A + k] : 0.0f;
+        const int na = a.R - a.D8 - 4;  // a multiple of 4
+        const float* sa = act_s + t * a.A;
+        for (int k = 0; k < na; k += 4)
+          *(f32x4*)(r + a.D8 + 4 + k) = (f32x4){k < a.A ? sa[k] : 0.f, k + 1 < a.A ? sa[k + 1] : 0.f,
+                                                k + 2 < a.A ? sa[k + 2] : 0.f, k + 3 < a.A ? sa[k + 3] : 0.f};
       }
     }
     __syncthreads();
