@@ -488,9 +488,27 @@ std::atomic<int64_t> g_targets_ringed{0};
 
 }  // namespace
 
+namespace dppo {
+bool perm_targets_parallel(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
+}
+
+// The serial draw (permpar.cpp falls back to it).
+int dppo_perm_targets_serial(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out) {
+  if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
+  MT g;
+  g.load(key, *pos);
+  draw_targets(g, n, count, out);
+  std::memcpy(key, g.mt, sizeof(g.mt));
+  *pos = g.pos;
+  return DPPO_OK;
+}
+
 extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
                                        int32_t* out) {
   if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
+  // large draws (C5's global minibatches: 4 x 8.4 M targets): the speculative chunked scan of
+  // permpar.cpp on DPPO_PERM_PAR_THREADS threads (default 8; 0 or 1 = this serial scan)
+  if (dppo::perm_targets_parallel(key, pos, n, count, out)) return DPPO_OK;
   MT g;
   g.load(key, *pos);
   // DPPO_PERM_TARGETS_RING=1 (A/B only): a producer thread twists the MT19937 blocks ahead of

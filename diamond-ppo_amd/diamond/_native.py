@@ -31,7 +31,7 @@ EXPORTED = [
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
+    "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
     "dppo_peer_export", "dppo_peer_open", "dppo_peer_close", "dppo_peer_allreduce",
     "dppo_peer_selftest",
@@ -133,6 +133,8 @@ def load():
         "dppo_get_trace": (ctypes.c_int, [vp, vp, i32]),
         "dppo_perm_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
         "dppo_perm_targets_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
+        "dppo_perm_targets_numpy_par": (ctypes.c_int, [vp, P(i32), i64, i32, vp, i32, vp, vp]),
+        "dppo_perm_par_stats": (ctypes.c_int, [P(i64)]),
         "dppo_perm_numpy_async": (ctypes.c_int, [vp, P(i32), i64, i32, vp, P(vp)]),
         "dppo_perm_wait": (ctypes.c_int, [vp]),
         "dppo_perm_stats": (ctypes.c_int, [P(i64)]),
@@ -241,6 +243,34 @@ def perm_targets_numpy(key: np.ndarray, pos: int, n: int, count: int,
     """The MT19937 half of :func:`perm_numpy`: Fisher-Yates swap targets ``out[c][i] = j_i``
     (the device resolves the swaps).  Advances ``key``/``pos`` exactly like perm_numpy."""
     return _mt_call("dppo_perm_targets_numpy", key, pos, n, count, out)
+
+
+PAR_STATS = ["path", "chunks", "records", "zone_words", "replayed_words", "max_offset", "W", "Wb",
+             "scan_us", "stitch_us", "assembly_us", "slowest_chunk_us", "words", "fail", "total_us",
+             "jump_us", "scalar_words", "triggers"]
+
+
+def perm_targets_numpy_par(key: np.ndarray, pos: int, n: int, count: int, out: np.ndarray,
+                           threads: int, chunks: int = 0, w: int = 0, w_mult: float = 0.0):
+    """:func:`perm_targets_numpy` split over ``threads`` threads (csrc/permpar.cpp), identical
+    results; returns (new pos, stats dict).  chunks / w / w_mult: the split and near-miss band
+    (tests force small ones to exercise every stitch path)."""
+    assert key.dtype == np.uint32 and key.size == 624 and key.flags.c_contiguous
+    assert out.dtype == np.int32 and out.size >= n * count and out.flags.c_contiguous
+    p = ctypes.c_int32(int(pos))
+    opts = np.array([chunks, w, int(round(w_mult * 100))], np.int64)
+    st = np.zeros(24, np.int64)
+    check(load().dppo_perm_targets_numpy_par(key.ctypes.data, ctypes.byref(p), int(n), int(count),
+                                             out.ctypes.data, int(threads), opts.ctypes.data,
+                                             st.ctypes.data), "dppo_perm_targets_numpy_par")
+    return int(p.value), {k: int(st[i]) for i, k in enumerate(PAR_STATS)}
+
+
+def perm_par_stats() -> dict:
+    """{attempts, parallel, fallback}: large draws through dppo_perm_targets_numpy so far."""
+    out = (ctypes.c_int64 * 3)()
+    check(load().dppo_perm_par_stats(out), "dppo_perm_par_stats")
+    return {"attempts": out[0], "parallel": out[1], "fallback": out[2]}
 
 
 def mt_state(rng=None):

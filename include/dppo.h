@@ -268,8 +268,28 @@ int dppo_perm_stats(int64_t* out3);
 
 /* The MT19937 half of dppo_perm_numpy: the Fisher-Yates swap targets out[c][i] = j_i
  * (i = n-1 .. 1; out[c][0] = 0) of `count` successive permutations, advancing key/pos exactly
- * as dppo_perm_numpy does.  Host only. */
+ * as dppo_perm_numpy does.  Host only.  Draws of >= 2^22 targets run the parallel form below on
+ * DPPO_PERM_PAR_THREADS threads (default 8; < 2 = serial). */
 int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
+
+/* The same draw split over `threads` threads (csrc/permpar.cpp: MT19937 jump-ahead, a
+ * speculative accept scan per chunk of the word stream, an exact serial stitch, a parallel
+ * assembly); identical outputs and key/pos advance.  Falls back to the serial draw (never to a
+ * different result) when a stitch check fails.  opts (nullable, 3 x int64): chunks (0 = threads),
+ * near-miss band W (0 = 6 sigma of the model), W multiplier x100 (0 = 600).  stats (nullable,
+ * 24 x int64): [0] path (0 serial, 1 parallel, 2 parallel attempt fell back), [1] chunks,
+ * [2] near-miss records, [3] kept zone words, [4] replayed words, [5] max |offset|, [6] W,
+ * [7] Wb, [8] scan us, [9] stitch us, [10] assembly us, [11] slowest chunk us, [12] words
+ * generated, [13] failure code, [14] total us, [15] slowest jump-ahead us, [16] words scanned
+ * one at a time, [17] disagreeing words applied.  Host only.
+ * Replaces the serial draw behind reference diamond/ppo.py:252-255 (np.random.permutation). */
+int dppo_perm_targets_numpy_par(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
+                                int32_t* out, int32_t threads, const int64_t* opts,
+                                int64_t* stats);
+
+/* Parallel-draw counters since load: {attempts by dppo_perm_targets_numpy, parallel draws
+ * completed, fallbacks to the serial draw}. */
+int dppo_perm_par_stats(int64_t* out3);
 
 /* The swap half on the device: perms[c] = arange(n) shuffled by targets[c] (device int32
  * [count][n]), identical to the sequential Fisher-Yates loop.  scratch: device int32

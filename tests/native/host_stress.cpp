@@ -120,6 +120,35 @@ void test_chained_async_drafts() {
   CHECK(std::memcmp(key, rkey, sizeof(key)) == 0 && pos == rpos);
 }
 
+// The parallel speculative draw (permpar.cpp) from several threads at once: the shared worker
+// pool, the chunk-buffer free list, a forced fallback (tiny near-miss band); every result equal
+// to the serial draw, generator state included.
+void test_parallel_draws() {
+  const int64_t n = (1 << 16) + 3;
+  const int count = 3;
+  std::vector<std::thread> th;
+  for (int t = 0; t < 3; ++t) {
+    th.emplace_back([t, n, count] {
+      for (int rep = 0; rep < 2; ++rep) {
+        const uint32_t seed = 700 + 10 * t + rep;
+        uint32_t rkey[624], key[624];
+        seed_key(seed, rkey);
+        std::memcpy(key, rkey, sizeof(key));
+        int32_t rpos = 624, pos = 624;
+        std::vector<int32_t> ref((size_t)(n * count)), out((size_t)(n * count));
+        int64_t st[24];
+        CHECK(dppo_perm_targets_numpy_par(rkey, &rpos, n, count, ref.data(), 1, nullptr, st) == 0);
+        const int64_t opts[3] = {6, rep == 1 && t == 0 ? 8 : 0, 0};  // 6 chunks; one tiny band
+        CHECK(dppo_perm_targets_numpy_par(key, &pos, n, count, out.data(), 4, opts, st) == 0);
+        CHECK(st[0] == (rep == 1 && t == 0 ? 2 : 1));
+        CHECK(out == ref);
+        CHECK(std::memcmp(key, rkey, sizeof(key)) == 0 && pos == rpos);
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
 void test_loop_barrier() {
   using dppo::LoopSync;
   {  // many generations, 4 ranks
@@ -182,6 +211,7 @@ int main() {
   setenv("DPPO_PERM_PIN", "3", 1);  // the pinned swap pool in any container
   test_concurrent_blocking_draws();
   test_chained_async_drafts();
+  test_parallel_draws();
   test_loop_barrier();
   int64_t st[3];
   dppo_perm_stats(st);

@@ -169,6 +169,59 @@ def test_host_swap_targets_replay_to_numpy_permutation(n):
         assert np.array_equal(closed_form_shuffle(j), ref[c])
 
 
+# (n, count, chunks, near-miss band W: 0 = the model's): tiny and odd sizes, powers of two (band
+# changes at chunk edges), many short chunks, and a band too narrow for the guess errors (the
+# stitch must fall back to the serial draw, never return other targets)
+PAR_CASES = [(2, 1, 4, 0), (3, 5, 4, 0), (1000, 3, 4, 0), ((1 << 15) + 1, 4, 7, 0),
+             (1 << 16, 2, 16, 0), (200003, 3, 5, 0), (200003, 3, 5, 40), ((1 << 17) - 1, 1, 3, 0)]
+
+
+@pytest.mark.parametrize("n,count,chunks,w", PAR_CASES)
+def test_parallel_draw_is_the_serial_draw(n, count, chunks, w):
+    """dppo_perm_targets_numpy_par (csrc/permpar.cpp: jump-ahead, speculative chunk scans, exact
+    stitch) returns exactly the serial draw's targets and MT19937 key / pos, from a fresh seed
+    (pos 624) and from mid-block positions."""
+    for seed, skip in ((5, 0), (6, 33), (7, 623)):
+        rs = np.random.RandomState(seed + n)
+        rs.random_sample(skip)
+        key, pos, _ = N.mt_state(rs)
+        ref = np.empty(n * count, np.int32)
+        k1 = key.copy()
+        p1, st1 = N.perm_targets_numpy_par(k1, pos, n, count, ref, 1)
+        assert st1["path"] == 0
+        got = np.full(n * count, -7, np.int32)
+        k2 = key.copy()
+        p2, st = N.perm_targets_numpy_par(k2, pos, n, count, got, 4, chunks=chunks, w=w)
+        assert np.array_equal(got, ref) and p2 == p1 and np.array_equal(k2, k1), st
+        if w:
+            assert st["path"] == 2 and st["fail"] != 0      # the narrow band is detected
+        elif n * count >= 1 << 16:
+            assert st["path"] == 1 and st["fail"] == 0, st  # the parallel draw itself ran
+
+
+def test_large_draws_take_the_parallel_path():
+    """dppo_perm_targets_numpy at >= 2^22 targets runs the parallel draw by default; targets equal
+    the serial draw's and the RNG ends where numpy's own permutations leave it."""
+    n, count = (1 << 20) + 1, 4
+    np.random.seed(2024)
+    key, pos, _ = N.mt_state()
+    before = N.perm_par_stats()
+    tg = np.empty(n * count, np.int32)
+    k1 = key.copy()
+    p1 = N.perm_targets_numpy(k1, pos, n, count, tg)
+    after = N.perm_par_stats()
+    assert after["attempts"] == before["attempts"] + 1
+    assert after["parallel"] == before["parallel"] + 1
+    ref = np.empty(n * count, np.int32)
+    k2 = key.copy()
+    p2, _ = N.perm_targets_numpy_par(k2, pos, n, count, ref, 1)
+    assert np.array_equal(tg, ref) and p1 == p2 and np.array_equal(k1, k2)
+    for _ in range(count):
+        np.random.permutation(n)
+    st = np.random.get_state()
+    assert np.array_equal(k1, st[1]) and p1 == st[2]
+
+
 def fisher_yates(j):
     a = np.arange(len(j))
     for i in range(len(j) - 1, 0, -1):

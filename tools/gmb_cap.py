@@ -2,15 +2,18 @@
 """Scaling cap of the reference-exact multi-GPU mode (cfg.global_minibatches = True) at BASELINE
 configs[4] (65,536 CartPole envs in total, strong scaling): every rank draws the reference's E
 permutations of the GLOBAL batch (T x 65,536 = 8.4 M samples, E = 4: 33.5 M Fisher-Yates targets,
-one sequential MT19937 accept scan -- ppo.py:252-255) while its device share shrinks as 1/world.
+ppo.py:252-255) and resolves them on its device, while its share of the learn shrinks as 1/world.
 
-For world = 1, 2, 4, 8: the host draw time per learn (dppo_perm_targets_numpy, the draw the
-device-shuffle path uses at these sizes; median of 3) and -- on a GPU box -- the device time per
-learn of one rank's share (T x 65,536/world envs, local minibatches, the same kernels).  The
-look-ahead drafts overlap the draws with the device, so a learn takes max(draw, device); the
-cap is device(1) / max(draw, device(world)).
+For world = 1, 2, 4, 8:
+* host draw per learn: the serial accept scan (perm.cpp) and the parallel speculative draw
+  (permpar.cpp, DPPO_PERM_PAR_THREADS threads; what dppo_perm_targets_numpy runs), median of 5;
+* on a GPU box: the device time per learn of one rank's share (T x 65,536/world envs, local
+  minibatches, the same kernels) plus the device work every rank repeats in global mode -- the
+  Fisher-Yates resolution of all E x 8.4 M targets (the "perm" kernels of the one-GPU C5 learn).
+The look-ahead drafts overlap the draw with the device, so a learn takes
+max(draw, share + resolution); the cap is device(1) / that.
 
-    python tools/gmb_cap.py [--no-gpu]
+    python tools/gmb_cap.py [--no-gpu] [--out file.json]
 """
 import argparse
 import json
@@ -25,16 +28,17 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "diamond-ppo_amd"))
 
 
-def host_draw_ms(n, epochs=4, reps=3):
+def host_draw_ms(n, epochs=4, reps=5, threads=1):
     from diamond import _native as N
     out = np.empty(n * epochs, np.int32)
     ts = []
-    for r in range(reps):
+    for r in range(reps + 1):
         rs = np.random.RandomState(42 + r)
         key, pos, _ = N.mt_state(rs)
         t0 = time.perf_counter()
-        N.perm_targets_numpy(key, pos, n, epochs, out)
-        ts.append((time.perf_counter() - t0) * 1e3)
+        N.perm_targets_numpy_par(key, pos, n, epochs, out, threads)
+        if r:  # the first draw is a warm-up (buffers, jump polynomials)
+            ts.append((time.perf_counter() - t0) * 1e3)
     return float(np.median(ts))
 
 
@@ -42,10 +46,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
     T, Ng = 128, 65536
-    draw = host_draw_ms(T * Ng)
-    dev = {}
+    threads = int(os.environ.get("DPPO_PERM_PAR_THREADS", "8"))
+    draw_serial = host_draw_ms(T * Ng)
+    draw_par = host_draw_ms(T * Ng, threads=threads)
+    dev, resolve = {}, None
     if not a.no_gpu:
         import torch
         import bench
@@ -56,16 +63,26 @@ def main():
                                    Ng // world, 4, 2, False, 0.02, 0.005, "weak")
             r = bench.run_config(name, 1, 0, None, device, a.steps, 2)
             dev[world] = r["device_ms_per_step"]
+            if world == 1:  # the one-GPU learn resolves all 4 x 8.4 M targets on the device
+                k = r["kernels"].get("perm")
+                resolve = k["ms_total"] / a.steps if k else None
+                dev[1] = r["device_ms_per_step"]
     rows = []
     for world in (1, 2, 4, 8):
-        row = {"world": world, "host_draw_ms_per_learn": round(draw, 2),
+        row = {"world": world, "host_draw_ms_serial": round(draw_serial, 2),
+               "host_draw_ms_parallel": round(draw_par, 2), "draw_threads": threads,
                "global_samples": T * Ng, "targets_drawn": 4 * T * Ng}
         if dev:
-            d = dev[world]
-            row["device_ms_per_learn_per_rank"] = d
-            row["learn_ms_bound"] = round(max(draw, d), 3)
-            row["host_bound"] = draw > d
-            row["speedup_cap_vs_1gpu"] = round(dev[1] / max(draw, d), 2)
+            share = dev[world] - (resolve if world == 1 else 0.0)
+            rdev = share + (resolve or 0.0)  # every rank resolves the global permutations
+            row["device_ms_share_local"] = round(share, 3)
+            row["device_ms_resolution"] = round(resolve or 0.0, 3)
+            row["device_ms_per_learn_global"] = round(rdev, 3)
+            for tag, draw in (("serial", draw_serial), ("parallel", draw_par)):
+                bound = max(draw, rdev)
+                row[f"learn_ms_bound_{tag}_draw"] = round(bound, 3)
+                row[f"speedup_cap_{tag}_draw"] = round(dev[1] / bound, 2)
+            row["host_bound_parallel_draw"] = draw_par > rdev
         rows.append(row)
     import platform
     cpu = platform.processor()
@@ -76,7 +93,11 @@ def main():
                 break
     except OSError:
         pass
-    print(json.dumps({"cpu": cpu, "rows": rows}), flush=True)
+    res = {"cpu": cpu, "rows": rows}
+    print(json.dumps(res), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
 
 
 if __name__ == "__main__":

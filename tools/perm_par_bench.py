@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Host draw of the reference-exact permutation targets at BASELINE configs[4] with global
+minibatches (E = 4 permutations of T x 65,536 = 8,388,608 samples: ppo.py:252-255), serial
+(perm.cpp) against the parallel speculative draw (permpar.cpp) at several thread counts.
+Every parallel draw is checked bit for bit (targets, MT19937 key and pos) against the serial one.
+
+    python tools/perm_par_bench.py [--reps 5] [--threads 4,8,12,16] [--out file.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "diamond-ppo_amd"))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=128 * 65536)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--threads", default="4,8,12,16")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from diamond import _native as N
+    n, E = a.n, a.epochs
+    got = np.empty(n * E, np.int32)
+    rows = []
+    serial_ms = []
+    by_thr = {int(t): [] for t in a.threads.split(",")}
+    # the serial references first (one per rep), then each thread count as its own block after
+    # one untimed warm-up draw: a process keeps one configuration, and the chunk buffers (sized
+    # on first use) are reused from call to call
+    states = []
+    for rep in range(a.reps):
+        rs = np.random.RandomState(1234 + rep)
+        rs.random_sample(rep * 37)  # a pos other than 624
+        key, pos, _ = N.mt_state(rs)
+        k1 = key.copy()
+        r1 = np.empty(n * E, np.int32)
+        t0 = time.perf_counter()
+        p1, _ = N.perm_targets_numpy_par(k1, pos, n, E, r1, 1)
+        serial_ms.append((time.perf_counter() - t0) * 1e3)
+        states.append((key, pos, k1, p1, r1))
+    for thr in by_thr:
+        key, pos = states[0][0], states[0][1]
+        N.perm_targets_numpy_par(key.copy(), pos, n, E, got, thr)  # warm-up
+        for rep, (key, pos, k1, p1, r1) in enumerate(states):
+            k2 = key.copy()
+            t0 = time.perf_counter()
+            p2, st = N.perm_targets_numpy_par(k2, pos, n, E, got, thr)
+            ms = (time.perf_counter() - t0) * 1e3
+            ok = bool(p1 == p2 and np.array_equal(k1, k2) and np.array_equal(r1, got))
+            by_thr[thr].append(ms)
+            st.update({"threads": thr, "rep": rep, "ms": round(ms, 3), "bit_exact": ok})
+            rows.append(st)
+            print(json.dumps(st), flush=True)
+            if not ok:
+                raise SystemExit(f"MISMATCH at threads={thr} rep={rep}")
+    med = lambda x: round(float(np.median(x)), 3)
+    summary = {"cpu": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)),
+               "n": n, "epochs": E, "targets": E * (n - 1),
+               "serial_ms_median": med(serial_ms),
+               "parallel_ms_median": {t: med(v) for t, v in by_thr.items()},
+               "parallel_ms_min": {t: round(min(v), 3) for t, v in by_thr.items()},
+               "fallbacks": sum(1 for r in rows if r["path"] != 1),
+               "all_bit_exact": all(r["bit_exact"] for r in rows)}
+    print(json.dumps(summary), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"summary": summary, "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
