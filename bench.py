@@ -212,22 +212,40 @@ def _baseline_inputs(cfg_name, seed=0):
     return (obs, nobs, act, rew, te, tr), params, names, cont, T * N
 
 
+def host_cpus():
+    """(CPUs the process may run on, CPUs its cgroup quota pays for or None, threads to use).
+    On the GPU box the affinity mask holds the whole machine (256) while the cgroup quota is the
+    box's share (16): more threads than the quota only get throttled."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return aff, quota, min(aff, quota) if quota else aff
+
+
 def cpu_baselines(cfg_name):
     """One full learn() of the same workload on the host cores: the PyTorch-CPU restatement
     (oracle/ppo_torch.py: the reference's own arithmetic -- autograd, torch.distributions,
-    clip_grad_norm_, CPU Adam -- at torch's intra-op thread count) and the NumPy oracle."""
+    clip_grad_norm_, CPU Adam) and the NumPy oracle.  Runs in a child process that never touches
+    the GPU (see cpu_baselines_child), on every CPU the process may use."""
     from oracle import ppo_np as P
     from oracle import ppo_torch as PT
     exp, params, names, cont, B = _baseline_inputs(cfg_name)
     model = PT.cpu_model()
-    threads = torch.get_num_threads()
+    aff, quota, threads = host_cpus()
+    torch.set_num_threads(threads)
     p1 = {k: v.copy() for k, v in params.items()}
     torch.optim.Adam([torch.zeros(1, requires_grad=True)])  # first-use imports outside the clock
     t0 = time.perf_counter()
     PT.learn(p1, exp, P.Hyper(), 3e-4, cont, rng=np.random.RandomState(42))
     dt_t = time.perf_counter() - t0
     torch_b = {"value": round(B / dt_t, 1), "unit": "env-steps/s", "cores": int(threads),
-               "kind": "port", "cpu": model,
+               "kind": "port", "cpu": model, "affinity_cpus": aff, "cgroup_cpus": quota,
+               "process": "child started before any GPU call (no HIP runtime, no draw threads)",
                "sample": f"one full learn() of {cfg_name} (T x N = {B} samples: old-policy eval, "
                          f"GAE, 4x8 minibatch autograd/clip/Adam steps) by the PyTorch-CPU "
                          f"restatement of the reference path (oracle/ppo_torch.py), {dt_t:.2f} s "
@@ -248,6 +266,18 @@ def cpu_baselines(cfg_name):
                "sample": f"the same learn() by the NumPy float32 oracle (oracle/ppo_np.py), "
                          f"{dt_n:.2f} s", "seconds": round(dt_n, 3)}
     return torch_b, numpy_b
+
+
+def cpu_baselines_child(cfg_name):
+    """Time cpu_baselines in a fresh interpreter started before this process makes any GPU call:
+    the baseline is then not slowed by the HIP runtime's threads or the permutation pools."""
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", cfg_name],
+                       capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
+    tb, nb = json.loads(r.stdout.strip().splitlines()[-1])
+    return tb, nb
 
 
 def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=True,
@@ -434,7 +464,12 @@ def main():
                     help="N = 1: skip the other BASELINE configs (C3, C4, C5 on one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel HIP events in the timed region (no roofline)")
+    ap.add_argument("--cpu-baseline-child", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_baseline_child:  # the baseline child: CPU only, prints one JSON line
+        sys.path.insert(0, ROOT)
+        print(json.dumps(cpu_baselines(args.cpu_baseline_child)), flush=True)
+        return
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -445,6 +480,11 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # first, before this process touches the GPU: the CPU path on the headline workload
+        # itself (c5's 65,536 envs: its 4,096-env shape)
+        baseline = cpu_baselines_child(args.config if args.config != "c5" else "cartpole4096")
     # DPPO_BENCH_REHEARSE=1: rehearse the N > 1 path on a one-GPU box -- every rank on GPU 0, a
     # gloo process group, the peer exchange between the ranks (RCCL refuses two ranks on one
     # device).  The numbers then measure ranks sharing one GPU, not scaling.
@@ -509,9 +549,8 @@ def main():
         # C5's one-GPU buffer (65,536 envs, 184 MB per launch): the launch ramp amortised
         out["roofline_gae_65536"] = {"exact": gae_roofline(device, N=65536),
                                      "affine": gae_roofline(device, N=65536, mode=1)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the CPU path on the headline workload itself (c5's 65,536 envs: its 4,096-env shape)
-        tb, nb = cpu_baselines(args.config if args.config != "c5" else "cartpole4096")
+    if baseline is not None:
+        tb, nb = baseline
         out["cpu_baseline"] = tb
         out["cpu_baseline_numpy"] = nb
         out["speedup_vs_cpu_baseline"] = round(out["value"] / tb["value"], 1)
