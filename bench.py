@@ -144,18 +144,28 @@ def gae_roofline(device, T=128, N=8192, sets=None, reps=4, mode=0):
     def launch(b):
         NN.check(h.lib.dppo_gae_f32(h.h, *[x.data_ptr() for x in b], 0.99, 0.95, s.cuda_stream))
 
+    def probe(b):  # the same bytes, no recurrence (dppo_gae_stream_probe): the launch's ceiling
+        NN.check(h.lib.dppo_gae_stream_probe(h.h, *[x.data_ptr() for x in b], s.cuda_stream),
+                 "dppo_gae_stream_probe")
+
     for b in bufs:
         launch(b)
+        probe(b)
     torch.cuda.synchronize(device)
     h.set_timing(True)
-    for _ in range(reps):
+    for _ in range(reps):  # alternating rounds over the same rotating sets
         for b in bufs:
             launch(b)
-    ms, cnt = h.timing()["gae"]
+        for b in bufs:
+            probe(b)
+    tm = h.timing()
+    ms, cnt = tm["gae"]
+    pms, pcnt = tm["gae_probe"]
     h.set_timing(False)
     per = ms / cnt
     nbytes = 22 * T * N
     achieved = nbytes / (per * 1e-3) / 1e9
+    ceil_us = pms / pcnt * 1e3
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     key = f"gae{N}" + ("_affine" if mode else "")
@@ -173,7 +183,12 @@ def gae_roofline(device, T=128, N=8192, sets=None, reps=4, mode=0):
             "mode": "affine (<= 1e-6 of scale)" if mode else "exact (bit-exact serial)",
             "num_envs": N, "rollout_steps": T,
             "bytes_per_launch": nbytes, "us_per_launch": round(per * 1e3, 2),
-            "launches": cnt, "rotating_sets": sets}
+            "launches": cnt, "rotating_sets": sets,
+            # the same bytes with no recurrence (dppo_gae_stream_probe), timed in the same run
+            # over the same sets: what one launch of these bytes streams at on this part
+            "ceiling_us": round(ceil_us, 2),
+            "ceiling_GBps": round(nbytes / (ceil_us * 1e-6) / 1e9, 1),
+            "frac_of_ceiling": round(ceil_us / (per * 1e3), 4)}
 
 
 def _gae_tile(N):
@@ -281,7 +296,7 @@ def cpu_baselines_child(cfg_name):
 
 
 def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=True,
-               global_mb=False):
+               global_mb=False, keep_agent=False):
     """Time `steps` learn() calls of CONFIGS[name] on this rank; returns the measurement dict
     (max wall time over ranks)."""
     import diamond
@@ -416,10 +431,88 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "perm_lookahead_hits": hits,
         "final_loss": float(loss_trace[-1, 0]),
     }
+    if keep_agent:
+        res["_agent"] = agent
     del agent, ro
     torch.cuda.synchronize(device)
     torch.cuda.empty_cache()
     return res
+
+
+def exchange_report(agent, dist, device, reps=200):
+    """The per-minibatch gradient exchange of a data-parallel learner: the transport engine
+    selected (peer exchange over the ranks' xGMI-mapped buffers, or RCCL), its start-up
+    self-test, the exchange buffer's memory type, and microseconds per gradient-sized exchange
+    (P + 8 floats, `reps` back to back on the launch stream, HIP events; max over ranks)."""
+    L = agent._learner
+    h = L.handle
+    n = h.layout.total + 8
+    buf = torch.zeros(n, dtype=torch.float32, device=device)
+    s = torch.cuda.current_stream(device)
+    peer = bool(getattr(L, "peer", False))
+    if peer:
+        f = lambda: h.peer_allreduce(buf.data_ptr(), n, False, s.cuda_stream)
+    else:
+        f = lambda: dist.all_reduce(buf)
+    for _ in range(10):
+        f()
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        f()
+    b.record(s)
+    b.synchronize()
+    us = a.elapsed_time(b) * 1e3 / reps
+    t = torch.tensor([us], dtype=torch.float64,
+                     device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    info = h.peer_info() if peer else {}
+    return {"transport": "peer" if peer else "rccl",
+            "peer_selftest": getattr(L, "peer_status", "not run"),
+            "memory": info.get("memory"), "fused_in_optimizer_step": info.get("fused"),
+            "bytes_per_exchange": 4 * n, "us_per_exchange_max_over_ranks": round(float(t.item()), 2),
+            "exchanges_timed": reps}
+
+
+def multi_gpu_report(world, rank, dist, device, steps, warmup):
+    """At N > 1, after the headline line's weak-scaling workload: BASELINE configs[4] as a
+    STRONG-scaling run (65,536 envs split over the ranks) in both minibatch modes -- local-union
+    (each rank permutes its own samples) and global (the reference's permutations of the whole
+    batch, ppo.py:252-255, reproduced on every rank) -- with update-steps/s (the north star's
+    >= 6x quantity) against a world-1 anchor measured on rank 0's GPU in the same job, and the
+    exchange transport with its self-test outcome and latency."""
+    from diamond import engine as EN
+    keys = ("value", "update_steps_per_s", "ms_per_step", "device_ms_per_step",
+            "host_work_ms_per_step", "host_ms_per_step")
+    rep = {}
+    for gmb in (False, True):
+        r = run_config("c5", world, rank, dist, device, steps, warmup, global_mb=gmb,
+                       keep_agent=True)
+        agent = r.pop("_agent")
+        row = {k: r[k] for k in keys}
+        row["num_envs_per_gpu"] = r["config"]["num_envs_per_gpu"]
+        row["minibatches"] = r["config"]["minibatches"]
+        perm = r["kernels"].get("perm")
+        row["perm_device_ms_per_step"] = round(perm["ms_total"] / steps, 4) if perm else 0.0
+        if not gmb:
+            rep["exchange"] = exchange_report(agent, dist, device)
+        rep["c5_strong_" + ("global" if gmb else "local")] = row
+        del agent
+        torch.cuda.empty_cache()
+    anchor = None
+    if rank == 0:  # the same learn on ONE GPU (the other ranks wait)
+        with EN.solo():
+            r1 = run_config("c5", 1, 0, None, device, steps, warmup, kernel_timing=False)
+        anchor = {k: r1[k] for k in ("update_steps_per_s", "value", "ms_per_step")}
+    dist.barrier()
+    if anchor is not None:
+        rep["c5_world1_anchor"] = anchor
+        rep["c5_update_steps_speedup_vs_world1"] = {
+            m: round(rep[f"c5_strong_{m}"]["update_steps_per_s"] / anchor["update_steps_per_s"], 3)
+            for m in ("local", "global")}
+    return rep
 
 
 def spawn_ranks(n: int) -> int:
@@ -461,7 +554,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gae-roofline", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
-                    help="N = 1: skip the other BASELINE configs (C3, C4, C5 on one GPU)")
+                    help="N = 1: skip the other BASELINE configs (C2, C4, C5 on one GPU); N > 1: "
+                         "skip the multi_gpu legs (C5 strong scaling, both minibatch modes, "
+                         "world-1 anchor, exchange latency)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="diagnostic: no per-kernel HIP events in the timed region (no roofline)")
     ap.add_argument("--cpu-baseline-child", default=None, help=argparse.SUPPRESS)
@@ -529,6 +624,10 @@ def main():
         out["device"] = {"name": torch.cuda.get_device_name(device),
                          "arch": getattr(torch.cuda.get_device_properties(device), "gcnArchName", ""),
                          "compute_units": torch.cuda.get_device_properties(device).multi_processor_count}
+    if world > 1 and not args.no_extra:
+        mg = multi_gpu_report(world, rank, dist, device, min(args.steps, 10), 2)
+        if rank == 0:
+            out["multi_gpu"] = mg
     if world == 1 and not args.no_extra:
         # the other BASELINE configs on this GPU (C3, C4), and C5's 65,536 global envs on ONE
         # GPU: the anchor of the configs[4] strong-scaling curve (`--config c5 --gpus N`)

@@ -165,6 +165,7 @@ struct dppo_handle {
   int xworld = 0;                    // > 0: the exchange carries every all-reduce
   bool xfused = false;               // the gradient exchange runs inside reduce_adam_kernel
   unsigned xseq = 0;                 // exchanges so far (the same count on every rank)
+  int xmem = 0;                      // exchange buffer memory: 0 coarse, 1 fine-grained, 2 uncached
   unsigned long long xticks = 0;     // wait bound of one exchange (s_memrealtime ticks)
 };
 
@@ -238,6 +239,14 @@ unsigned next_radam_epoch(dppo_handle* h) {
   return h->radam_epoch;
 }
 
+// Test-only environment hooks (a sequence number near the 32-bit wrap, a skewed self-test
+// contribution) act only with DPPO_TEST_HOOKS=1, so a stray variable cannot change a production
+// run.
+const char* test_hook(const char* name) {
+  const char* e = std::getenv("DPPO_TEST_HOOKS");
+  return e && e[0] == '1' ? std::getenv(name) : nullptr;
+}
+
 template <typename T>
 int dalloc(T** p, int64_t n) {
   if (n <= 0) n = 1;
@@ -280,7 +289,8 @@ int device_status(const dppo_handle* h) {
 }
 
 enum KClass {
-  K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_PERM, K_RADAM, K_NCLASS
+  K_EVAL = 0, K_GAE, K_STATS, K_PACK, K_GRAD, K_REDUCE, K_ADAM, K_COMM, K_PERM, K_RADAM, K_PROBE,
+  K_NCLASS
 };
 
 hipEvent_t pool_event(dppo_handle* h) {
@@ -464,8 +474,16 @@ int prepare(dppo_handle* h, const dppo_rollout* ro, const float* params, const d
   // (4) advantage statistics, global over ranks (ppo.py:243).  One rank: the pack kernel reduces
   // the GAE partials itself (one launch and one kernel boundary fewer per learn); several: the
   // reduced sums are all-reduced first.  DPPO_STATS_LAUNCH=1 keeps the separate launch (A/B).
-  static const bool stats_launch = std::getenv("DPPO_STATS_LAUNCH") != nullptr;
-  const bool fold_stats = hp->advantage_norm && !distributed(h) && !stats_launch;
+  static const bool stats_launch = [] {
+    const char* e = std::getenv("DPPO_STATS_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  // Folded only where the partials are few (the persistent GAE kernels: one per workgroup, <= the
+  // CU count): every pack block re-reduces all of them, which on the fallback GAE path (N % 16 != 0
+  // or unaligned buffers: one partial per 16 envs, 4,096 at N = 65,536) would be ~128 MB of
+  // redundant L2 reads per learn -- there the separate reduction launch is cheaper.
+  const bool fold_stats =
+      hp->advantage_norm && !distributed(h) && !stats_launch && h->n_partials <= 512;
   if (hp->advantage_norm && !fold_stats) {
     {
       Timed tm(h, K_STATS, s);
@@ -978,6 +996,26 @@ int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, cons
                     &h->n_partials, h->gae_mode);
 }
 
+int dppo_gae_stream_probe(dppo_handle* h, const float* rewards, const uint8_t* term,
+                          const uint8_t* trunc, const float* values, const float* next_values,
+                          float* adv, float* returns, void* stream) {
+  if (!h || !rewards || !term || !trunc || !values || !next_values || !adv || !returns) {
+    set_error("null argument to dppo_gae_stream_probe");
+    return DPPO_EINVAL;
+  }
+  const int64_t n = (int64_t)h->dims.rollout_steps * h->dims.num_envs;
+  const uintptr_t al = (uintptr_t)rewards | (uintptr_t)values | (uintptr_t)next_values |
+                       (uintptr_t)adv | (uintptr_t)returns | (uintptr_t)term | (uintptr_t)trunc;
+  if (n % 4 != 0 || al % 16 != 0) {
+    set_error("dppo_gae_stream_probe: T*N must be a multiple of 4 and every buffer 16-B aligned");
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  Timed tm(h, K_PROBE, S(stream));
+  return launch_gae_stream_probe(rewards, term, trunc, values, next_values, adv, returns, n,
+                                 S(stream));
+}
+
 int dppo_set_gae_mode(dppo_handle* h, int32_t mode) {
   if (!h || (mode != DPPO_GAE_EXACT && mode != DPPO_GAE_AFFINE)) {
     set_error("invalid argument to dppo_set_gae_mode");
@@ -1322,14 +1360,32 @@ int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
                 (long long)cap, kPeerChunk * kPeerMaxSlices);
       return DPPO_EUNSUPPORTED;
     }
-    // a whole 2 MiB allocation of its own (IPC maps allocations, not sub-ranges of a pool)
+    // a whole 2 MiB allocation of its own (IPC maps allocations, not sub-ranges of a pool).
+    // DPPO_PEER_MEM: coarse (hipMalloc), fine (hipDeviceMallocFinegrained) or uncached
+    // (hipDeviceMallocUncached).  Peers poll these words across xGMI with system-scope loads;
+    // fine-grained / uncached memory is the type whose accesses from other agents the runtime
+    // declares coherent (no line of it kept in a reader's caches), see DESIGN.md §6.
     const int64_t bytes = (peer_buffer_bytes(cap) + (2 << 20) - 1) / (2 << 20) * (2 << 20);
-    DPPO_TRY(dalloc(&h->xbuf, bytes));
+    const char* mem = std::getenv("DPPO_PEER_MEM");
+    h->xmem = !mem ? 0 : (std::strcmp(mem, "fine") == 0 ? 1 : std::strcmp(mem, "uncached") == 0 ? 2 : 0);
+    if (h->xmem == 0) {
+      DPPO_TRY(dalloc(&h->xbuf, bytes));
+    } else {
+      const hipError_t e = hipExtMallocWithFlags((void**)&h->xbuf, (size_t)bytes,
+                                                 h->xmem == 1 ? hipDeviceMallocFinegrained
+                                                              : hipDeviceMallocUncached);
+      if (e != hipSuccess) {
+        h->xbuf = nullptr;
+        set_error("hipExtMallocWithFlags(%lld bytes, %s) failed: %s", (long long)bytes,
+                  h->xmem == 1 ? "fine-grained" : "uncached", hipGetErrorString(e));
+        return DPPO_ENOMEM;
+      }
+    }
     DPPO_HIP_CHECK(hipMemset(h->xbuf, 0, (size_t)bytes));
-    // DPPO_PEER_XSEQ0 (tests, dppo_peer_open): counting on from s0, the slice flags start as if
-    // exchange s0 had just completed -- the (wrap-safe) flag comparison needs flags within 2^31
-    // of the sequence, as they always are once exchanges have run
-    if (const char* x0 = std::getenv("DPPO_PEER_XSEQ0")) {
+    // DPPO_PEER_XSEQ0 (test hook, dppo_peer_open): counting on from s0, the slice flags start as
+    // if exchange s0 had just completed -- the (wrap-safe) flag comparison needs flags within
+    // 2^31 of the sequence, as they always are once exchanges have run
+    if (const char* x0 = test_hook("DPPO_PEER_XSEQ0")) {
       const unsigned s0 = (unsigned)std::strtoul(x0, nullptr, 0);
       for (int k = 0; k < kPeerMaxSlices; ++k)
         DPPO_HIP_CHECK(hipMemcpy(h->xbuf + 4 * cap * 8 + 64 * (int64_t)k, &s0, sizeof(s0),
@@ -1393,7 +1449,7 @@ int dppo_peer_open(dppo_handle* h, int32_t nranks, int32_t rank, const unsigned 
   h->xfused = !(flags & DPPO_PEER_SHARED_DEVICE) && !(fz && fz[0] == '0');
   // DPPO_PEER_XSEQ0 (tests): the exchange number to count on from, e.g. just below the 32-bit
   // wrap; every rank must set the same value
-  const char* x0 = std::getenv("DPPO_PEER_XSEQ0");
+  const char* x0 = test_hook("DPPO_PEER_XSEQ0");
   if (x0) h->xseq = (unsigned)std::strtoul(x0, nullptr, 0);
   h->xworld = nranks;
   h->nranks = nranks;
@@ -1417,6 +1473,18 @@ int dppo_peer_close(dppo_handle* h) {
     h->nranks = h->dims.world_size;
     h->rank = h->dims.rank;
   }
+  return DPPO_OK;
+}
+
+int dppo_peer_info(dppo_handle* h, int64_t* out4) {
+  if (!h || !out4) {
+    set_error("invalid argument to dppo_peer_info");
+    return DPPO_EINVAL;
+  }
+  out4[0] = h->xworld;
+  out4[1] = h->xworld > 0 && h->xfused && h->radam_ok ? 1 : 0;
+  out4[2] = h->xbuf ? h->xmem : -1;
+  out4[3] = (int64_t)h->xseq;
   return DPPO_OK;
 }
 
@@ -1467,7 +1535,7 @@ int dppo_peer_selftest(dppo_handle* h, void* stream) {
     }
     // DPPO_PEER_SELFTEST_SKEW=r (tests): rank r contributes one wrong element to exchange 0, as
     // a rank reading stale or incoherent peer memory would see it
-    const char* skew = std::getenv("DPPO_PEER_SELFTEST_SKEW");
+    const char* skew = test_hook("DPPO_PEER_SELFTEST_SKEW");
     const int skew_rank = skew ? std::atoi(skew) : -1;
     for (int k = 0; k < 4; ++k) {
       for (int64_t i = 0; i < n; ++i)

@@ -89,6 +89,8 @@ __device__ __forceinline__ f32x2 tanh2(f32x2 x) {
 }
 
 // Launchers implemented in the .hip files (all stream-ordered, no host sync).
+int launch_gae_stream_probe(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
+                            const float* nv, float* adv, float* ret, int64_t n, hipStream_t s);
 int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
                const float* nv, float* adv, float* ret, double* partials, int T, int N,
                float gamma, float gae_lambda, hipStream_t s, int* n_partials,

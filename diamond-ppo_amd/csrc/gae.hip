@@ -207,6 +207,21 @@ struct PipeLds {
   int scanned[kPChunks];
 };
 
+// LDS row swizzle of the env-major operand rows: element (env, t) of a super-chunk lives at
+// column t ^ pswz(env).  Rows are 132 floats apart (16-B aligned for the scan's ds_read_b128), so
+// without it the owners' 4-B writes -- lane (env 4m + j, row) -- land 4 lanes per bank at 64-env
+// tiles and 2 at 32 (rocprofv3: 63.8 % / 36 % bank-conflict cycles).  XOR by 12 x (env >> 4 & 3)
+// keeps every 4-row group contiguous and aligned, is constant over each 16-env group of the scan
+// (whose 16-B reads stay conflict-free), and makes the owners' writes and reads conflict-free at
+// 16-, 32- and 64-env tiles (bank model over every lane pattern of the kernel).
+__device__ __forceinline__ int pswz(int env) {
+#ifdef DPPO_GAE_NOSWZ
+  return 0 * env;
+#else
+  return 12 * ((env >> 4) & 3);
+#endif
+}
+
 __device__ __forceinline__ void gae_terms(float r, float v, float nv, float te, float tr, float g,
                                           float c, float& delta, float& coef) {
 #pragma clang fp contract(off)
@@ -310,6 +325,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     // first (latest in time) is requested first and tends to land first
     const int k = kPChunks - 1 - wave;
     const int e0 = 4 * (lane % V4);
+    const int sw = pswz(e0);  // the same for e0 .. e0 + 3
     double lsum = 0.0, lsq = 0.0;
     int gen = 0;
     // Staggered start of the first tile's loads: owner w (chunk 7 - w) issues `stagger` cycles
@@ -353,15 +369,15 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
               float d, cf;
               gae_terms(xr[p][j], xv[p][j], xn[p][j], ((xt[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f,
                         ((xu[p] >> (8 * j)) & 0xffu) ? 1.0f : 0.0f, g, c, d, cf);
-              L.delta[e0 + j][r0 + row] = d;
-              L.coef[e0 + j][r0 + row] = cf;
+              L.delta[e0 + j][(r0 + row) ^ sw] = d;
+              L.coef[e0 + j][(r0 + row) ^ sw] = cf;
             }
           } else {
             // rows past the end of the rollout: a = -0 + 1 * a is the identity for every a
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              L.delta[e0 + j][r0 + row] = -0.0f;
-              L.coef[e0 + j][r0 + row] = 1.0f;
+              L.delta[e0 + j][(r0 + row) ^ sw] = -0.0f;
+              L.coef[e0 + j][(r0 + row) ^ sw] = 1.0f;
             }
           }
         }
@@ -379,7 +395,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
           const int row = p * RP + lane / V4;
           if (row < nr) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) avp[p][j] = L.a[e0 + j][r0 + row];
+            for (int j = 0; j < 4; ++j) avp[p][j] = L.a[e0 + j][(r0 + row) ^ sw];
           }
         }
 #pragma unroll
@@ -419,6 +435,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     // previous chunk (with one chunk of look-ahead it did: ~650 cycles per 16-step chunk under
     // the owners' LDS traffic, against ~250 now).
     const int e = lane;
+    const int sw = pswz(e);
     int gen = 0;
     // The scan is the youngest wave of the workgroup and shares its SIMD with two owners: at the
     // default priority every owner VALU instruction issues first (age order) and the dependent
@@ -435,8 +452,8 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
         auto fetch = [&](int k, int set) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            d[set][q] = *(const f32x4*)&L.delta[e][k * kPChunk + 4 * q];
-            cf[set][q] = *(const f32x4*)&L.coef[e][k * kPChunk + 4 * q];
+            d[set][q] = *(const f32x4*)&L.delta[e][(k * kPChunk + 4 * q) ^ sw];
+            cf[set][q] = *(const f32x4*)&L.coef[e][(k * kPChunk + 4 * q) ^ sw];
           }
         };
         // Wait for chunk k by polling its flag and its data together: the flag read is performed
@@ -493,7 +510,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
               av[j >> 2][j & 3] = a;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][k * kPChunk + 4 * q] = av[q];
+            for (int q = 0; q < 4; ++q) *(f32x4*)&L.a[e][(k * kPChunk + 4 * q) ^ sw] = av[q];
 #endif
           };
           if (pf[k] < gen) {  // prefetched before its owner published it: poll and re-read
@@ -1041,6 +1058,47 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
   else
     DPPO_LAUNCH(gae_kernel<false>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv,
                        ret, partials, T, N, gamma, c);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+// ---- The streaming ceiling of the GAE launch (measurement only, dppo_gae_stream_probe): the
+// same 22 B per element over the same [T][N] buffers -- read rewards, values, next_values (16 B
+// per lane) and the two flag bytes, write advantages and returns -- with no recurrence, one
+// persistent grid like gae_pipe_kernel's.  What one launch of these bytes reaches on this part
+// (bench.py roofline_gae: ceiling_us, frac_of_ceiling).
+__global__ __launch_bounds__(256) void gae_stream_probe_kernel(
+    const float* __restrict__ r, const uint8_t* __restrict__ te, const uint8_t* __restrict__ tr,
+    const float* __restrict__ v, const float* __restrict__ nv, float* __restrict__ adv,
+    float* __restrict__ ret, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const f32x4 a = ((const f32x4*)r)[i];
+    const f32x4 b = ((const f32x4*)v)[i];
+    f32x4 o = ((const f32x4*)nv)[i];
+    const uint32_t t = ((const uint32_t*)te)[i];
+    const uint32_t u = ((const uint32_t*)tr)[i];
+    o[0] += (float)((t ^ u) & 0xffu);
+    ((f32x4*)adv)[i] = a + b;
+    ((f32x4*)ret)[i] = o;
+  }
+}
+
+int launch_gae_stream_probe(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
+                            const float* nv, float* adv, float* ret, int64_t n, hipStream_t s) {
+  if (n <= 0) return DPPO_OK;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  const int64_t n4 = n / 4;
+  int64_t grid = (n4 + 255) / 256;
+  if (grid > 4 * cus) grid = 4 * cus;  // 1,024 on 256 CUs: the probe's best (profiles/r02_*)
+  DPPO_LAUNCH(gae_stream_probe_kernel, dim3((unsigned)grid), dim3(256), 0, s, r, te, tr, v, nv,
+              adv, ret, n4);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

@@ -784,6 +784,20 @@ struct Stitch {
     C->lits.push_back((int32_t)v);
     ++kt;
   }
+  // up to 16 literals at once: the accepted lanes of v, in lane order
+  PAR_AVX512 void literals(__m512i v, __mmask16 acc, int cnt) {
+    if (!cnt) return;
+    const size_t base = C->lits.size();
+    C->lits.resize(base + 16);
+    _mm512_storeu_si512((void*)(C->lits.data() + base), _mm512_maskz_compress_epi32(acc, v));
+    C->lits.resize(base + (size_t)cnt);
+    if (!C->ops.empty() && C->ops.back().lit && C->ops.back().k + C->ops.back().len == kt &&
+        C->ops.back().src + C->ops.back().len == (int64_t)base)
+      C->ops.back().len += cnt;
+    else
+      C->ops.push_back(Op{kt, (int64_t)base, cnt, 1});
+    kt += cnt;
+  }
   // no disagreement up to guessed index s2: the copy extends
   void advance_to(int64_t s2) {
     kt += s2 - s;
@@ -871,7 +885,7 @@ struct Stitch {
 };
 
 // Runs the stitch over all chunks; fills ops / lits; returns false on any failed check.
-bool stitch_all(Draw& D, Stitch& X) {
+PAR_AVX512 bool stitch_all(Draw& D, Stitch& X) {
   enum { OFFSET, EXACT, LOCKED } mode = OFFSET;
   int64_t kt = 0;
   for (size_t c = 0; c < D.ch.size(); ++c) {
@@ -1052,13 +1066,45 @@ bool stitch_all(Draw& D, Stitch& X) {
       X.s = kgq - C.kg0;
       X.flush();
       run_set(D, X.tr, X.kt);
-      Run gr;  // the guessed run, followed through its accept bits
-      run_set(D, gr, kgq);
       const uint32_t* rw = C.raw.data() + z.raw0 - z.q0;
       const int64_t bo = z.raw0 - z.q0;
       bool back = false;
       int64_t x = q;
-      for (; x < (int64_t)z.q1; ++x) {
+      while (x < (int64_t)z.q1) {
+        // 16 words at once where the true run can neither change band, finish, nor meet an
+        // ambiguous word (the scan's group step); the guessed counter advances by the popcount
+        // of its 16 accept bits
+        if (!X.tr.done && x + 16 <= (int64_t)z.q1 && X.tr.i >= X.tr.lo + 15 &&
+            X.tr.k + 16 < D.K) {
+          const uint32_t ii = X.tr.i;
+          const __m512i v = _mm512_and_si512(_mm512_loadu_si512((const void*)(rw + x)),
+                                             _mm512_set1_epi32((int)X.tr.mask));
+          const __mmask16 acc = _mm512_cmple_epu32_mask(v, _mm512_set1_epi32((int)(ii - 15)));
+          const __mmask16 le = _mm512_cmple_epu32_mask(v, _mm512_set1_epi32((int)ii));
+          if (!(le & ~acc)) {
+            const int cnt = __builtin_popcount((unsigned)acc);
+            X.literals(v, acc, cnt);
+            X.tr.k += cnt;
+            X.tr.i -= (uint32_t)cnt;
+            if (X.tr.i < X.tr.lo) {
+              X.tr.mask = smear(X.tr.i);
+              X.tr.lo = (X.tr.mask >> 1) + 1;
+            }
+            const int64_t b = x + bo;
+            const int o = (int)(b & 63);
+            uint64_t w16 = C.bits[(size_t)(b >> 6)] >> o;
+            if (o > 48) w16 |= C.bits[(size_t)(b >> 6) + 1] << (64 - o);
+            const int gcnt = __builtin_popcountll(w16 & 0xFFFFull);
+            kgq += gcnt;
+            x += 16;
+            X.exact_words += 16;
+            if ((cnt || gcnt) && D.band(kgq) == D.band(X.kt)) {
+              back = true;
+              break;
+            }
+            continue;
+          }
+        }
         ++X.exact_words;
         bool moved = false;
         if (!X.tr.done) {
@@ -1076,12 +1122,11 @@ bool stitch_all(Draw& D, Stitch& X) {
         }
         if ((C.bits[(size_t)((x + bo) >> 6)] >> ((x + bo) & 63)) & 1) {
           ++kgq;
-          run_accept(D, gr);
           moved = true;
         }
-        if (moved && same_band(X.tr, gr)) {
+        ++x;
+        if (moved && D.band(kgq) == D.band(X.kt)) {
           back = true;
-          ++x;
           break;
         }
       }

@@ -194,10 +194,40 @@ int fy_grid(int64_t total) {
 
 }  // namespace
 
+int launch_perm_resolve_one(const int32_t* targets, int32_t* perms, int64_t n, int32_t* scratch,
+                            hipStream_t s) {
+  int32_t* head = scratch;
+  int32_t* nxt = scratch + n;
+  int32_t* mq = scratch + 2 * n;
+  DPPO_HIP_CHECK(hipMemsetAsync(head, 0xFF, (size_t)n * sizeof(int32_t), s));
+  const int G = fy_grid(n);
+  DPPO_LAUNCH(fy_build_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, n, n);
+  DPPO_LAUNCH_CHECK();
+  DPPO_LAUNCH(fy_links_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, mq, perms, n, n);
+  DPPO_LAUNCH_CHECK();
+  DPPO_LAUNCH(fy_solve_kernel, dim3(G), dim3(kBlock), 0, s, targets, mq, perms, n, n);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
 int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
                         int32_t* scratch, hipStream_t s) {
   const int64_t total = n * (int64_t)count;
   if (total == 0) return DPPO_OK;
+  // DPPO_PERM_EPOCHWISE=1 (A/B): one epoch at a time, so the random accesses of the three passes
+  // (heads, links, chains: ~134 MB per 8.4 M-entry epoch) stay within the 256 MB Infinity Cache
+  // instead of spanning all epochs' 536 MB at C5
+  static const bool epochwise = [] {
+    const char* e = std::getenv("DPPO_PERM_EPOCHWISE");
+    return e && e[0] == '1';
+  }();
+  if (epochwise && count > 1) {
+    for (int32_t c = 0; c < count; ++c) {
+      const int rc = launch_perm_resolve_one(targets + c * n, perms + c * n, n, scratch, s);
+      if (rc != DPPO_OK) return rc;
+    }
+    return DPPO_OK;
+  }
   int32_t* head = scratch;
   int32_t* nxt = scratch + total;
   int32_t* mq = scratch + 2 * total;

@@ -26,19 +26,19 @@ PERM_SLOTS = 3  # pinned permutation staging slots per handle (include/dppo.h DP
 
 EXPORTED = [
     "dppo_version", "dppo_last_error", "dppo_param_layout", "dppo_create", "dppo_destroy",
-    "dppo_gae_f32", "dppo_set_gae_mode", "dppo_adv_stats", "dppo_adv_sums", "dppo_adv_stats_from_sums",
+    "dppo_gae_f32", "dppo_gae_stream_probe", "dppo_set_gae_mode", "dppo_adv_stats", "dppo_adv_sums", "dppo_adv_stats_from_sums",
     "dppo_adv_normalize_f32", "dppo_old_policy_f32",
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
     "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
-    "dppo_peer_export", "dppo_peer_open", "dppo_peer_close", "dppo_peer_allreduce",
+    "dppo_peer_export", "dppo_peer_open", "dppo_peer_close", "dppo_peer_allreduce", "dppo_peer_info",
     "dppo_peer_selftest",
     "dppo_gru_param_layout", "dppo_gru_create", "dppo_gru_destroy", "dppo_gru_minibatch_grad_f32",
 ]
 TIMING_CLASSES = ["eval", "gae", "adv_stats", "pack", "grad", "slab_reduce", "clip_adam",
-                  "allreduce", "perm", "reduce_adam"]
+                  "allreduce", "perm", "reduce_adam", "gae_probe"]
 
 
 class Dims(ctypes.Structure):
@@ -113,6 +113,7 @@ def load():
         "dppo_destroy": (None, [vp]),
         "dppo_gae_f32": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, vp]),
         "dppo_adv_stats": (ctypes.c_int, [vp, vp, vp]),
+        "dppo_gae_stream_probe": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "dppo_set_gae_mode": (ctypes.c_int, [vp, i32]),
         "dppo_adv_normalize_f32": (ctypes.c_int, [vp, vp, i64, vp]),
         "dppo_adv_sums": (ctypes.c_int, [vp, vp, vp]),
@@ -145,6 +146,7 @@ def load():
         "dppo_peer_export": (ctypes.c_int, [vp, vp]),
         "dppo_peer_open": (ctypes.c_int, [vp, i32, i32, vp, i32]),
         "dppo_peer_close": (ctypes.c_int, [vp]),
+        "dppo_peer_info": (ctypes.c_int, [vp, P(i64)]),
         "dppo_peer_allreduce": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "dppo_peer_selftest": (ctypes.c_int, [vp, vp]),
         "dppo_status": (ctypes.c_int, [vp]),
@@ -379,6 +381,13 @@ class Handle:
 
     def peer_close(self):
         check(self.lib.dppo_peer_close(self.h), "dppo_peer_close")
+
+    def peer_info(self) -> dict:
+        """{ranks, fused, memory, exchanges} of this handle's peer exchange (dppo_peer_info)."""
+        out = (ctypes.c_int64 * 4)()
+        check(self.lib.dppo_peer_info(self.h, out), "dppo_peer_info")
+        mem = {0: "coarse-grained", 1: "fine-grained", 2: "uncached", -1: None}[out[2]]
+        return {"ranks": out[0], "fused": bool(out[1]), "memory": mem, "exchanges": out[3]}
 
     def peer_allreduce(self, ptr: int, n: int, f64: bool, stream):
         check(self.lib.dppo_peer_allreduce(self.h, ptr, int(n), int(bool(f64)), stream),

@@ -54,9 +54,23 @@ def require_gpu(cfg_device_index: int = 0) -> torch.device:
     return torch.device("cuda", idx)
 
 
+_SOLO = [False]
+
+
+class solo:
+    """``with engine.solo():`` agents built inside ignore an initialised torch.distributed group
+    and run as one rank (bench.py measures its world-1 anchor on rank 0 inside an N-rank job)."""
+
+    def __enter__(self):
+        _SOLO[0] = True
+
+    def __exit__(self, *exc):
+        _SOLO[0] = False
+
+
 def dist_world():
     d = torch.distributed
-    if d.is_available() and d.is_initialized():
+    if not _SOLO[0] and d.is_available() and d.is_initialized():
         return d.get_world_size(), d.get_rank()
     return 1, 0
 
@@ -405,7 +419,8 @@ class NativeLearner:
         mode = os.environ.get("DPPO_COMM", "auto")
         if mode not in ("auto", "rccl", "peer"):
             raise ValueError(f"DPPO_COMM={mode!r}: expected auto, rccl or peer")
-        if not (d.is_available() and d.is_initialized()):   # one rank, no process group
+        self.peer_status = "not run"
+        if _SOLO[0] or not (d.is_available() and d.is_initialized()):   # one rank, no group
             if mode == "peer":   # (DPPO_FORCE_COMM=1: the 1-rank exchange, measurements)
                 h = self.handle
                 err = h.peer_open(1, 0, h.peer_export()) or h.peer_selftest(
@@ -446,19 +461,30 @@ class NativeLearner:
         """Map every rank's exchange buffer and run one checked exchange; every rank keeps the
         peer exchange only if every rank succeeded (ranks must never disagree on the transport)."""
         h = self.handle
-        me = (h.peer_export(), self._gpu_identity())
+        # test hooks (DPPO_TEST_HOOKS=1, csrc/capi.cpp test_hook) must agree across ranks: a
+        # sequence start that differs between ranks would stall every exchange
+        hooks = ((os.environ.get("DPPO_PEER_XSEQ0"), os.environ.get("DPPO_PEER_SELFTEST_SKEW"))
+                 if os.environ.get("DPPO_TEST_HOOKS") == "1" else None)
+        me = (h.peer_export(), self._gpu_identity(), hooks)
         mine = [None] * self.world
         d.all_gather_object(mine, me)
         gpus = [m[1] for m in mine]
-        err = h.peer_open(self.world, self.rank, b"".join(m[0] for m in mine),
-                          shared_device=len(set(gpus)) < len(gpus))
+        if len({m[2][0] if m[2] else None for m in mine}) > 1:
+            err = "DPPO_PEER_XSEQ0 differs across ranks"
+        else:
+            err = h.peer_open(self.world, self.rank, b"".join(m[0] for m in mine),
+                              shared_device=len(set(gpus)) < len(gpus))
         if self._all_ranks(d, not err):
             err = h.peer_selftest(torch.cuda.current_stream(self.device).cuda_stream)
             if self._all_ranks(d, not err):
+                self.peer_status = "passed"
                 return True
             h.peer_close()
-        elif not err:
-            h.peer_close()
+            self.peer_status = f"self-test failed: {err or 'on another rank'}"
+        else:
+            if not err:
+                h.peer_close()
+            self.peer_status = f"mapping failed: {err or 'on another rank'}"
         msg = f"peer exchange unavailable on rank {self.rank}: {err or 'another rank failed'}"
         if required:
             raise RuntimeError(msg)

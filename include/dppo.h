@@ -137,6 +137,14 @@ int dppo_gae_f32(dppo_handle* h, const float* rewards, const uint8_t* term, cons
  * re-associated fp32, <= 1e-6 of the advantages' scale from the reference). */
 int dppo_set_gae_mode(dppo_handle* h, int32_t mode);
 
+/* Measurement only (no reference counterpart): the streaming ceiling of dppo_gae_f32 -- the same
+ * 22 bytes per element over the same buffers (reads rewards, values, next_values, term, trunc;
+ * writes adv and returns with meaningless values), no recurrence, one persistent grid.  Timed
+ * like the GAE kernel (dppo_set_timing, class "gae_probe").  T*N % 4 == 0, 16-B aligned buffers. */
+int dppo_gae_stream_probe(dppo_handle* h, const float* rewards, const uint8_t* term,
+                          const uint8_t* trunc, const float* values, const float* next_values,
+                          float* adv, float* returns, void* stream);
+
 /* Mean and unbiased std of the advantages of the last dppo_gae_f32 (ppo.py:243, reduced over
  * all ranks when a communicator is attached); writes device float mean_std[2]. */
 int dppo_adv_stats(dppo_handle* h, float* mean_std, void* stream);
@@ -326,6 +334,10 @@ int dppo_peer_close(dppo_handle* h);
  * The advantage statistics use the stand-alone exchange kernel.
  * every rank's `n` values summed in rank order into buf, in place (f64 != 0: doubles) */
 int dppo_peer_allreduce(dppo_handle* h, void* buf, int64_t n, int32_t f64, void* stream);
+/* The handle's peer exchange: out4 = {ranks (0 = none), gradient exchange fused into the
+ * optimizer kernel (0/1), exchange-buffer memory (0 coarse-grained, 1 fine-grained, 2 uncached;
+ * -1 = not allocated; DPPO_PEER_MEM), exchanges so far}. */
+int dppo_peer_info(dppo_handle* h, int64_t* out4);
 /* one exchange of a known pattern (f32 and f64) checked exactly; synchronous */
 int dppo_peer_selftest(dppo_handle* h, void* stream);
 

@@ -44,8 +44,11 @@ def _spawn(kind, tmp_path, world=2, env=None):
 
 
 @pytest.mark.timeout(300)
-def test_peer_exchange_two_ranks_learn_matches_single_gpu(tmp_path):
-    r0, r1 = _spawn("handle", tmp_path)
+@pytest.mark.parametrize("mem", ["coarse", "fine", "uncached"])
+def test_peer_exchange_two_ranks_learn_matches_single_gpu(tmp_path, mem):
+    """Two processes on this GPU, each mapping the other's exchange buffer (hipIpc), for every
+    exchange-buffer memory type (DPPO_PEER_MEM: hipMalloc, fine-grained, uncached)."""
+    r0, r1 = _spawn("handle", tmp_path, env={"DPPO_PEER_MEM": mem})
     print(f"peer exchange, 2 ranks on one GPU: {float(r0['us_per_exchange']):.2f} us per "
           f"gradient-sized exchange (rank 1: {float(r1['us_per_exchange']):.2f})")
     for gmb in (0, 1):
@@ -63,7 +66,7 @@ def test_peer_exchange_across_the_sequence_wrap(tmp_path):
     """The exchange numbers wrap at 2^32 (0 is reserved) and the buffers are double-buffered by
     parity: counting on from 0xFFFFFFF0, the self-test and both learns cross the wrap and must
     still give identical parameters on both ranks, equal to the world-1 learn."""
-    r0, r1 = _spawn("handle", tmp_path, env={"DPPO_PEER_XSEQ0": str(0xFFFFFFF0)})
+    r0, r1 = _spawn("handle", tmp_path, env={"DPPO_PEER_XSEQ0": str(0xFFFFFFF0), "DPPO_TEST_HOOKS": "1"})
     for gmb in (0, 1):
         assert np.array_equal(r0[f"params{gmb}"], r1[f"params{gmb}"]), gmb
         np.testing.assert_allclose(r0[f"params{gmb}"], r0[f"single{gmb}"], rtol=0, atol=5e-6)
@@ -88,7 +91,7 @@ def test_failing_peer_selftest_is_refused_on_every_rank(tmp_path):
     required (DPPO_COMM=peer), every agent construction raises; under DPPO_COMM=auto the same
     agreement falls back to RCCL (tests/test_comm_agreement_cpu.py: RCCL refuses two ranks on
     this box's one GPU)."""
-    rs = _spawn("selftest_fail", tmp_path, env={"DPPO_PEER_SELFTEST_SKEW": "1"})
+    rs = _spawn("selftest_fail", tmp_path, env={"DPPO_PEER_SELFTEST_SKEW": "1", "DPPO_TEST_HOOKS": "1"})
     assert "expected" in str(rs[0]["err"]) or "another rank failed" in str(rs[0]["err"])
     for r in rs:
         assert "peer exchange unavailable" in str(r["err"]), str(r["err"])
@@ -103,13 +106,20 @@ def test_peer_exchange_drop_in_agent(tmp_path):
     assert np.array_equal(r0["trace"], r1["trace"])
 
 
-def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces():
+@pytest.mark.parametrize("variant", ["coarse", "fine", "wrap"])
+def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(monkeypatch, variant):
     """A 1-rank peer exchange in this process: every learn() then takes the multi-rank sequence
     of a node with one GPU per rank -- the advantage statistics through the exchange kernel, and
     each minibatch's gradient exchange INSIDE reduce_adam_kernel (publish the block's slice, wait
     for every rank's flag, sum in rank order) -- and must reproduce the reference's captured
     traces.  (Two ranks sharing this GPU take the unfused exchange: their optimizer-step grids
-    could not be resident at once; the test above.)"""
+    could not be resident at once; the test above.)  Variants: the exchange buffer fine-grained,
+    and the fused exchange counting on from just below the 2^32 sequence wrap (test hook)."""
+    if variant == "fine":
+        monkeypatch.setenv("DPPO_PEER_MEM", "fine")
+    if variant == "wrap":
+        monkeypatch.setenv("DPPO_TEST_HOOKS", "1")
+        monkeypatch.setenv("DPPO_PEER_XSEQ0", str(0xFFFFFFF0))
     import diamond
     from conftest import load_golden
     from gpu_helpers import stream
@@ -122,6 +132,10 @@ def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces():
         h = L.handle
         assert not h.peer_open(1, 0, h.peer_export())
         assert not h.peer_selftest(stream())
+        info = h.peer_info()
+        assert info["ranks"] == 1 and info["fused"], info
+        assert info["memory"] == ("fine-grained" if variant == "fine" else "coarse-grained")
+        seq0 = info["exchanges"]
         h.set_timing(True)
         losses, norms = [], []
         for li in range(n_learn):
@@ -138,6 +152,8 @@ def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces():
         E, M = int(z["cfg/num_epochs"]), int(z["cfg/num_minibatches"])
         assert tm["allreduce"][1] == n_learn, tm                 # advantage statistics only
         assert tm["reduce_adam"][1] == n_learn * E * M and tm["clip_adam"][1] == 0, tm
+        if variant == "wrap":  # the fused exchanges crossed the wrap (0 is skipped)
+            assert seq0 >= 0xFFFFFFF0 and h.peer_info()["exchanges"] < seq0, (seq0, h.peer_info())
         np.testing.assert_allclose(losses, z["loss"], rtol=2e-5, atol=2e-5, err_msg=name)
         np.testing.assert_allclose(norms, z["norm"], rtol=2e-5, atol=2e-5, err_msg=name)
         for n, p in agent.network.named_parameters():
@@ -185,3 +201,17 @@ def test_bench_gpus_flag_starts_the_ranks_itself():
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0
     assert d["config"]["name"] == "lunar8192" and d["config"]["num_envs_total"] == 2 * 8192
     assert d["config"]["exchange"] == "peer"
+    # every multi-GPU question of the north star from this one invocation: configs[4] strong
+    # scaling in both minibatch modes against a world-1 anchor, and the exchange itself
+    mg = d["multi_gpu"]
+    ex = mg["exchange"]
+    assert ex["transport"] == "peer" and ex["peer_selftest"] == "passed"
+    assert ex["us_per_exchange_max_over_ranks"] > 0 and ex["memory"] in (
+        "coarse-grained", "fine-grained", "uncached")
+    for m in ("local", "global"):
+        row = mg[f"c5_strong_{m}"]
+        assert row["num_envs_per_gpu"] == 65536 // 2 and row["update_steps_per_s"] > 0
+        assert row["minibatches"] == ("global" if m == "global" else "local-union")
+        assert mg["c5_update_steps_speedup_vs_world1"][m] > 0
+    assert mg["c5_strong_global"]["perm_device_ms_per_step"] > 0
+    assert mg["c5_world1_anchor"]["update_steps_per_s"] > 0

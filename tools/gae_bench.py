@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--sets", type=int, default=16)
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--affine", action="store_true", help="the affine-scan (tolerance) mode")
+    ap.add_argument("--with-probe", action="store_true",
+                    help="after every GAE sweep, the same sweep of dppo_gae_stream_probe (the "
+                         "no-recurrence ceiling over the same buffers)")
     a = ap.parse_args()
     T, N = a.T, a.N
     dev = torch.device("cuda", 0)
@@ -71,11 +74,19 @@ def main():
         sweeps.append((e0, e1))
     torch.cuda.synchronize()
     sw_ms = np.array([x.elapsed_time(y) for x, y in sweeps]) / a.sets
+    def probe(b):
+        NN.check(h.lib.dppo_gae_stream_probe(h.h, *[x.data_ptr() for x in b], s.cuda_stream),
+                 "dppo_gae_stream_probe")
+
     h.set_timing(True)
     for _ in range(a.reps):
         for b in bufs:
             launch(b)
-    kms, kcnt = h.timing()["gae"]
+        if a.with_probe:
+            for b in bufs:
+                probe(b)
+    tm = h.timing()
+    kms, kcnt = tm["gae"]
     h.set_timing(False)
     nbytes = 22 * T * N
     out = {"T": T, "N": N, "staged": bool(os.environ.get("DPPO_GAE_STAGED")),
@@ -86,6 +97,10 @@ def main():
            "GBps_kernel_events": round(nbytes / (kms / kcnt * 1e-3) / 1e9, 1),
            "GBps_event_pair": round(nbytes / (np.median(per_ms) * 1e-3) / 1e9, 1),
            "GBps_sweep": round(nbytes / (np.median(sw_ms) * 1e-3) / 1e9, 1)}
+    if a.with_probe:
+        pms, pcnt = tm["gae_probe"]
+        out["us_probe_kernel_events"] = round(pms / pcnt * 1e3, 2)
+        out["frac_of_ceiling"] = round(pms / pcnt / (kms / kcnt), 4)
     print(json.dumps(out), flush=True)
 
 
