@@ -634,12 +634,20 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
   DPPO_TRY(upload_perms(h, host_buf, targets ? h->targets_dev2[ds] : h->perms_dev, ds));
   DPPO_TRY(prepare(h, rollout, params, hp, outputs, s));
   DPPO_HIP_CHECK(hipStreamWaitEvent(s, h->perms_ready, 0));
-  if (targets) {
+  if (targets && h->gmb && perm_walk()) {
+    // global minibatches from the swap targets: only this rank's samples are walked to their
+    // positions (the whole permutation is never resolved; perms_dev holds the marks)
+    Timed tm(h, K_PERM, s);
+    DPPO_TRY(launch_shard_select_targets(h->targets_dev2[ds], h->perms_dev, h->perm_scratch,
+                                         h->perms_local, h->seg, h->sel_cnt, h->Bg,
+                                         d.num_envs * h->nranks, d.num_envs * h->rank,
+                                         d.num_envs, (int32_t)E, (int32_t)M, s));
+  } else if (targets) {
     Timed tm(h, K_PERM, s);
     DPPO_TRY(launch_perm_resolve(h->targets_dev2[ds], h->perms_dev, h->pe, (int32_t)E,
                                  h->perm_scratch, s));
   }
-  if (h->gmb) {
+  if (h->gmb && !(targets && perm_walk())) {
     // this rank's members of every global minibatch, in permutation order
     Timed tm(h, K_PERM, s);
     DPPO_TRY(launch_shard_select(h->perms_dev, h->perms_local, h->seg, h->sel_cnt, h->Bg,
@@ -1220,6 +1228,33 @@ int dppo_learn_targets_f32(dppo_handle* h, const dppo_rollout* rollout, float* p
   return learn_impl(h, rollout, params, adam_m, adam_v, hp, host_targets, true, outputs, stream);
 }
 
+int dppo_global_minibatch_lists(dppo_handle* h, const int32_t* targets, int32_t* local,
+                                int32_t* seg, void* stream) {
+  if (!h || !targets || !local || !seg || !h->gmb) {
+    set_error("dppo_global_minibatch_lists: needs a global_minibatches handle of world_size > 1 "
+              "and device targets / local / seg buffers");
+    return DPPO_EINVAL;
+  }
+  const dppo_dims& d = h->dims;
+  if (h->Bg % d.num_minibatches != 0) {
+    set_error("dppo_global_minibatch_lists: global batch %lld not divisible into %d minibatches",
+              (long long)h->Bg, d.num_minibatches);
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  Timed tm(h, K_PERM, S(stream));
+  if (perm_walk())
+    return launch_shard_select_targets(targets, h->perms_dev, h->perm_scratch, local, seg,
+                                       h->sel_cnt, h->Bg, d.num_envs * d.world_size,
+                                       d.num_envs * d.rank, d.num_envs, d.num_epochs,
+                                       d.num_minibatches, S(stream));
+  DPPO_TRY(launch_perm_resolve(targets, h->perms_dev, h->Bg, d.num_epochs, h->perm_scratch,
+                               S(stream)));
+  return launch_shard_select(h->perms_dev, local, seg, h->sel_cnt, h->Bg,
+                             d.num_envs * d.world_size, d.num_envs * d.rank, d.num_envs,
+                             d.num_epochs, d.num_minibatches, S(stream));
+}
+
 int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
                       int32_t* scratch, void* stream) {
   if (!targets || !perms || !scratch || n < 0 || n > 0x7FFFFFFF || count < 0) {
@@ -1361,13 +1396,14 @@ int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
       return DPPO_EUNSUPPORTED;
     }
     // a whole 2 MiB allocation of its own (IPC maps allocations, not sub-ranges of a pool).
-    // DPPO_PEER_MEM: coarse (hipMalloc), fine (hipDeviceMallocFinegrained) or uncached
-    // (hipDeviceMallocUncached).  Peers poll these words across xGMI with system-scope loads;
-    // fine-grained / uncached memory is the type whose accesses from other agents the runtime
-    // declares coherent (no line of it kept in a reader's caches), see DESIGN.md §6.
+    // DPPO_PEER_MEM: uncached (hipDeviceMallocUncached, the default), fine
+    // (hipDeviceMallocFinegrained) or coarse (hipMalloc).  Peers poll these words across xGMI
+    // with system-scope loads; uncached memory is never held in any agent's L2, so a poll
+    // always reads the owner's HBM and a publish is visible once its store retires -- coherent
+    // across devices by construction, and measured no slower than coarse.
     const int64_t bytes = (peer_buffer_bytes(cap) + (2 << 20) - 1) / (2 << 20) * (2 << 20);
     const char* mem = std::getenv("DPPO_PEER_MEM");
-    h->xmem = !mem ? 0 : (std::strcmp(mem, "fine") == 0 ? 1 : std::strcmp(mem, "uncached") == 0 ? 2 : 0);
+    h->xmem = !mem ? 2 : (std::strcmp(mem, "fine") == 0 ? 1 : std::strcmp(mem, "coarse") == 0 ? 0 : 2);
     if (h->xmem == 0) {
       DPPO_TRY(dalloc(&h->xbuf, bytes));
     } else {

@@ -401,6 +401,13 @@ int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32
 // keep, in order, the samples of env shard [env0, env0 + Nl) as local indices t*Nl + (n - env0)
 // into local[E][T*Nl]; seg[E][M+1] = where each global minibatch (mbg samples) starts in the
 // epoch's list.  cnt: scratch of E * shard_select_chunks(T*Ng) ints.
+// Global minibatches straight from the swap targets: bucket build + a value walk of this rank's
+// samples only + the ordered selection (no whole-permutation resolution).  DPPO_PERM_WALK=0:
+// resolve + select instead (A/B).
+bool perm_walk();
+int launch_shard_select_targets(const int32_t* targets, int32_t* marks, int32_t* scratch,
+                                int32_t* local, int32_t* seg, int32_t* cnt, int64_t bg, int32_t ng,
+                                int32_t env0, int32_t nl, int32_t E, int32_t M, hipStream_t s);
 int shard_select_chunks(int64_t bg);
 int launch_shard_select(const int32_t* gperm, int32_t* local, int32_t* seg, int32_t* cnt,
                         int64_t bg, int32_t ng, int32_t env0, int32_t nl, int32_t E, int32_t M,

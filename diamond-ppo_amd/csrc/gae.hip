@@ -207,18 +207,19 @@ struct PipeLds {
   int scanned[kPChunks];
 };
 
-// LDS row swizzle of the env-major operand rows: element (env, t) of a super-chunk lives at
-// column t ^ pswz(env).  Rows are 132 floats apart (16-B aligned for the scan's ds_read_b128), so
-// without it the owners' 4-B writes -- lane (env 4m + j, row) -- land 4 lanes per bank at 64-env
-// tiles and 2 at 32 (rocprofv3: 63.8 % / 36 % bank-conflict cycles).  XOR by 12 x (env >> 4 & 3)
-// keeps every 4-row group contiguous and aligned, is constant over each 16-env group of the scan
-// (whose 16-B reads stay conflict-free), and makes the owners' writes and reads conflict-free at
-// 16-, 32- and 64-env tiles (bank model over every lane pattern of the kernel).
+// LDS row swizzle of the env-major operand rows (DPPO_GAE_SWZ builds only): element (env, t) of a
+// super-chunk at column t ^ 12 (env >> 4 & 3).  Rows are 132 floats apart (16-B aligned for the
+// scan's ds_read_b128), so the owners' 4-B writes -- lane (env 4m + j, row) -- land 4 lanes per
+// bank at 64-env tiles and 2 at 32.  The swizzle keeps every 4-row group contiguous and aligned
+// and the scan's reads conflict-free; measured (round 5, rocprofv3, 2 reps): bank-conflict share
+// at N = 65,536 62.3 % -> 35.8 %, but the launch 39.3 -> 41.0-43.2 us (the per-access XOR on the
+// owners' and the scan's addresses), and 8.0 -> 8.05-8.1 us at 8,192.  The conflicts are not on
+// the launch's critical path (it waits on the arrival of the loads, §3.2): off by default.
 __device__ __forceinline__ int pswz(int env) {
-#ifdef DPPO_GAE_NOSWZ
-  return 0 * env;
-#else
+#ifdef DPPO_GAE_SWZ
   return 12 * ((env >> 4) & 3);
+#else
+  return 0 * env;
 #endif
 }
 

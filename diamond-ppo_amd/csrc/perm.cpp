@@ -507,7 +507,7 @@ extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, i
                                        int32_t* out) {
   if (bad_args(key, pos, n, count, out)) return DPPO_EINVAL;
   // large draws (C5's global minibatches: 4 x 8.4 M targets): the speculative chunked scan of
-  // permpar.cpp on DPPO_PERM_PAR_THREADS threads (default 8; 0 or 1 = this serial scan)
+  // permpar.cpp on DPPO_PERM_PAR_THREADS threads (default 12; 0 or 1 = this serial scan)
   if (dppo::perm_targets_parallel(key, pos, n, count, out)) return DPPO_OK;
   MT g;
   g.load(key, *pos);

@@ -495,6 +495,19 @@ struct Draw {
   int P0 = 0;
   const uint32_t* key0 = nullptr;
   std::vector<int64_t> bounds;  // band changes (sorted), the draw's end K included
+  // overlap of the phases (par_draw): chunk c's scan done / its stitch done (null: sequential)
+  std::atomic<int>* scanned = nullptr;
+  std::atomic<int>* stitched = nullptr;
+  void wait_scanned(size_t c) const {
+    if (!scanned) return;
+    for (int k = 0; !scanned[c].load(std::memory_order_acquire); ++k)
+      if (k > 64) std::this_thread::yield();
+      else _mm_pause();
+  }
+  void mark_stitched(size_t c0, size_t c1) const {  // chunks [c0, c1)
+    if (!stitched) return;
+    for (size_t c = c0; c < c1; ++c) stitched[c].store(1, std::memory_order_release);
+  }
   Model model;
   std::vector<Chunk> ch;
 
@@ -889,6 +902,8 @@ PAR_AVX512 bool stitch_all(Draw& D, Stitch& X) {
   enum { OFFSET, EXACT, LOCKED } mode = OFFSET;
   int64_t kt = 0;
   for (size_t c = 0; c < D.ch.size(); ++c) {
+    D.wait_scanned(c);
+    if (c > 0) D.mark_stitched(c - 1, c);  // chunk c-1's ops are final
     Chunk& C = D.ch[c];
     X.C = &C;
     X.kt = kt;
@@ -924,6 +939,7 @@ PAR_AVX512 bool stitch_all(Draw& D, Stitch& X) {
           X.flush();
           X.end_word = C.Q0 + C.q_done;
           C.kt1 = X.kt;
+          D.mark_stitched(c, D.ch.size());
           return true;
         }
         X.advance_to(C.kg_end - C.kg0);
@@ -1115,6 +1131,7 @@ PAR_AVX512 bool stitch_all(Draw& D, Stitch& X) {
             if (X.tr.k == D.K) {
               X.end_word = C.Q0 + x + 1;
               C.kt1 = X.kt;
+              D.mark_stitched(c, D.ch.size());
               return true;
             }
             moved = true;
@@ -1158,12 +1175,19 @@ PAR_AVX512 bool stitch_all(Draw& D, Stitch& X) {
 // ------------------------------------------------------------------------------------------
 // Assembly and the worker pool
 // ------------------------------------------------------------------------------------------
-// dst[-j] = src[j], j < len
+// dst[-j] = src[j], j < len.  The destination (the pinned upload slot) is written with
+// non-temporal 64-B stores where aligned: no read-for-ownership of lines that are only written,
+// and the CPU caches are left to the scan.
 PAR_AVX512 void copy_reversed(int32_t* dst, const int32_t* src, int64_t len) {
   const __m512i rev = _mm512_set_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
   int64_t j = 0;
+  // head: until dst - j + 1 (the end of the next 16-element block) is 64-B aligned
+  while (j < len && (((uintptr_t)(dst - j + 1)) & 63) != 0) {
+    dst[-j] = src[j];
+    ++j;
+  }
   for (; j + 16 <= len; j += 16)
-    _mm512_storeu_si512((void*)(dst - j - 15),
+    _mm512_stream_si512((__m512i*)(dst - j - 15),
                         _mm512_permutexvar_epi32(rev, _mm512_loadu_si512((const void*)(src + j))));
   for (; j < len; ++j) dst[-j] = src[j];
 }
@@ -1192,6 +1216,31 @@ class Pool {
     static Pool* p = new Pool();  // leaked on purpose: no join at process exit
     return *p;
   }
+  // helpers (threads - 1 workers) run `body` while the caller does other work; wait() returns
+  // once every helper has left it.  One session at a time (the lock).
+  class Session {
+   public:
+    Session(Pool& p, int helpers, std::function<void()> body) : p_(p), lk_(p.run_mu_) {
+      p_.ensure(helpers);
+      std::lock_guard<std::mutex> g(p_.mu_);
+      p_.task_ = std::move(body);
+      p_.helpers_ = std::min(helpers, (int)p_.workers_.size());
+      p_.gen_++;
+      p_.cv_.notify_all();
+    }
+    void wait() {
+      std::unique_lock<std::mutex> g(p_.mu_);
+      // a helper that has not picked the task up yet must not start it late: clear it first
+      p_.task_ = nullptr;
+      p_.done_cv_.wait(g, [&] { return p_.active_ == 0; });
+    }
+    ~Session() { wait(); }
+
+   private:
+    Pool& p_;
+    std::lock_guard<std::mutex> lk_;
+  };
+
   // runs fn(0 .. jobs-1) on `threads` threads (the caller is one of them)
   void run(int jobs, int threads, const std::function<void(int)>& fn) {
     std::lock_guard<std::mutex> serial(run_mu_);
@@ -1309,7 +1358,7 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
   double Etot, Vtot;
   D.model.before(D.K, &Etot, &Vtot);
   // chunks: whole blocks, chunk c >= 1 starting at block c * Lb
-  const int64_t C = std::max<int64_t>(1, chunks > 0 ? chunks : threads);
+  const int64_t C = std::max<int64_t>(1, chunks > 0 ? chunks : 2 * (int64_t)threads);
   // whole blocks per chunk from the model alone (not from pos), so the jump polynomials --
   // x^(624 c Lb - 1) mod phi, ~25 squarings each -- are computed once per configuration
   int64_t Lb = (int64_t)(Etot / (kN * (double)C));
@@ -1382,18 +1431,59 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
     Wmax = std::max(Wmax, ch.W);
     Wbmax = std::max(Wbmax, ch.Wb);
   }
-  // phase 1: speculative scans
+  // The three phases overlap: the helpers scan chunks in order (then assemble), the caller
+  // stitches chunk c as soon as its scan is done, and a chunk is assembled as soon as its stitch
+  // is done.  With two chunks per thread the stitch of the first half runs under the scans of the
+  // second.
   const double t1 = now_us();
   field();  // build phi before the workers race for it
   const int64_t est = D.K / C + 1;
-  Pool::get().run((int)C, threads, [&](int c) {
-    scan_chunk(D, D.ch[(size_t)c], c == C - 1, c == C - 1 ? est + est / 4 : est);
-  });
-  const double t2 = now_us();
-  // phase 2: stitch
+  std::unique_ptr<std::atomic<int>[]> scanned(new std::atomic<int>[(size_t)C]);
+  std::unique_ptr<std::atomic<int>[]> stitched(new std::atomic<int>[(size_t)C]);
+  for (int64_t c = 0; c < C; ++c) {
+    scanned[c].store(0);
+    stitched[c].store(0);
+  }
+  D.scanned = scanned.get();
+  D.stitched = stitched.get();
+  std::atomic<int> next_scan{0}, next_asm{0}, abort_asm{0};
+  std::atomic<double> scans_done_at{0.0};
+  auto assemble_jobs = [&] {
+    for (int a; (a = next_asm.fetch_add(1)) < (int)C;) {
+      for (int k = 0; !stitched[a].load(std::memory_order_acquire); ++k) {
+        if (abort_asm.load(std::memory_order_relaxed)) return;
+        if (k > 64) std::this_thread::yield();
+        else _mm_pause();
+      }
+      if (abort_asm.load(std::memory_order_relaxed)) return;
+      const Chunk& ch = D.ch[(size_t)a];
+      if (!ch.ops.empty()) assemble_chunk(D, ch, out);
+      _mm_sfence();  // the non-temporal stores drained before the caller reads or uploads out
+    }
+  };
   Stitch X(D);
-  const bool ok = stitch_all(D, X);
-  const double t3 = now_us();
+  bool ok = false;
+  double t3 = 0;
+  {
+    Pool::Session ses(Pool::get(), threads - 1, [&] {
+      for (int c; (c = next_scan.fetch_add(1)) < (int)C;) {
+        scan_chunk(D, D.ch[(size_t)c], c == C - 1, c == C - 1 ? est + est / 4 : est);
+        scanned[c].store(1, std::memory_order_release);
+        double prev = scans_done_at.load(), t = now_us();
+        while (t > prev && !scans_done_at.compare_exchange_weak(prev, t)) {
+        }
+      }
+      assemble_jobs();
+    });
+    ok = stitch_all(D, X);
+    t3 = now_us();
+    if (ok) D.mark_stitched(0, (size_t)C);
+    else abort_asm.store(1);
+    // the caller helps with the last assemblies, then every helper has left the body
+    if (ok) assemble_jobs();
+    ses.wait();
+  }
+  const double t2 = scans_done_at.load() > 0 ? scans_done_at.load() : t3;
   int64_t recs = 0, zw = 0, gen = 0;
   double scan_max = 0, jump_max = 0;
   int64_t scal = 0;
@@ -1413,8 +1503,8 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
     st[5] = X.max_delta;
     st[6] = Wmax;
     st[7] = Wbmax;
-    st[8] = (int64_t)(t2 - t1);
-    st[9] = (int64_t)(t3 - t2);
+    st[8] = (int64_t)(t2 - t1);  // the last scan done
+    st[9] = (int64_t)(t3 - t1);  // the stitch done (it overlaps the scans)
     st[11] = (int64_t)scan_max;
     st[12] = gen;
     st[13] = ok ? 0 : X.fail;
@@ -1439,17 +1529,12 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
     if (st) st[13] = 7;
     return false;
   }
-  // phase 3: assembly
-  Pool::get().run((int)C, threads, [&](int c) {
-    const Chunk& ch = D.ch[(size_t)c];
-    if (!ch.ops.empty()) assemble_chunk(D, ch, out);
-  });
   for (int64_t e = 0; e < count; ++e) out[e * n] = 0;
   const double t4 = now_us();
   if (nkey != key) std::memcpy(key, nkey, kN * sizeof(uint32_t));
   *pos = npos;
   if (st) {
-    st[10] = (int64_t)(t4 - t3);
+    st[10] = (int64_t)(t4 - t3);  // assembly after the stitch
     st[14] = (int64_t)(t4 - t_start);
   }
   return true;
@@ -1462,7 +1547,7 @@ namespace dppo {
 bool perm_targets_parallel(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out) {
   static const int threads = [] {
     const char* e = std::getenv("DPPO_PERM_PAR_THREADS");
-    return e ? std::atoi(e) : 8;
+    return e ? std::atoi(e) : 12;
   }();
   static const int64_t min_targets = [] {
     const char* e = std::getenv("DPPO_PERM_PAR_MIN");

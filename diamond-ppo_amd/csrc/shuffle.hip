@@ -75,6 +75,65 @@ __device__ __forceinline__ int32_t root(const int32_t* __restrict__ mq, int64_t 
   return q;
 }
 
+// The value walk (the inverse form of the closed form above): value v starts at position q = v
+// with every step i >= n still to come.  The first step that touches position q is the LARGEST
+// step i in (q, bound) with j_i = q -- it moves v up to position i, which no later (smaller)
+// step can touch: final -- and otherwise step q itself, which moves v down to j_q (or leaves it:
+// j_q = q, final); from there only steps below the old q remain.  Positions strictly decrease, so
+// the walk ends; on random targets it takes ~2 hops of ~2 bucket entries each (NumPy
+// restatement: tests/test_native_cpu.py value_walk_positions).  A rank that needs the positions of only some values
+// (global minibatches: its own env shard) walks only those.
+__device__ __forceinline__ int32_t walk_pos(const int32_t* __restrict__ tgt,
+                                            const int32_t* __restrict__ head,
+                                            const int32_t* __restrict__ nxt, int64_t base,
+                                            int32_t n, int32_t v) {
+  int32_t q = v, bound = n;
+  for (;;) {
+    int32_t best = -1;
+    for (int32_t it = head[base + q]; it >= 0; it = nxt[base + it])
+      best = (it > q && it < bound && it > best) ? it : best;
+    if (best >= 0 || q == 0) return best >= 0 ? best : 0;
+    const int32_t jq = tgt[base + q];
+    if ((uint32_t)jq >= (uint32_t)q) return q;  // j_q == q (or an invalid target: stays)
+    bound = q;
+    q = jq;
+  }
+}
+
+// perms[c][pos(v)] = v for every value: the whole permutation (one GPU)
+__global__ __launch_bounds__(kBlock) void fy_walk_scatter_kernel(const int32_t* __restrict__ tgt,
+                                                                const int32_t* __restrict__ head,
+                                                                const int32_t* __restrict__ nxt,
+                                                                int32_t* __restrict__ perms,
+                                                                int64_t n, int64_t total) {
+  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * kBlock) {
+    const int64_t c = g / n;
+    const int32_t v = (int32_t)(g - c * n);
+    perms[c * n + walk_pos(tgt, head, nxt, c * n, (int32_t)n, v)] = v;
+  }
+}
+
+// marks[c][pos(v)] = l for this rank's values only: local sample l = t * nl + e of the shard
+// [env0, env0 + nl) is global sample v = t * ng + env0 + e (marks pre-filled with -1)
+__global__ __launch_bounds__(kBlock) void fy_walk_mark_kernel(const int32_t* __restrict__ tgt,
+                                                             const int32_t* __restrict__ head,
+                                                             const int32_t* __restrict__ nxt,
+                                                             int32_t* __restrict__ marks,
+                                                             int64_t n, int64_t b_local,
+                                                             int32_t E, int32_t ng, int32_t env0,
+                                                             int32_t nl) {
+  const int64_t total = b_local * E;
+  for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * kBlock) {
+    const int64_t c = g / b_local;
+    const int32_t l = (int32_t)(g - c * b_local);
+    const int32_t t = l / nl;
+    const int32_t v = t * ng + env0 + (l - t * nl);
+    marks[c * n + walk_pos(tgt, head, nxt, c * n, (int32_t)n, v)] = l;
+  }
+}
+
 // out aliases succ (each thread reads its own succ before overwriting it)
 __global__ __launch_bounds__(kBlock) void fy_solve_kernel(const int32_t* __restrict__ tgt,
                                                          const int32_t* __restrict__ mq,
@@ -113,6 +172,14 @@ __device__ __forceinline__ bool in_shard(int32_t i, int32_t ng, int32_t env0, in
   return (uint32_t)(i - t * ng - env0) < (uint32_t)nl;
 }
 
+// MARK: the source is a marks array (>= 0: this rank's local sample at that position) instead of
+// the global permutation
+template <bool MARK>
+__device__ __forceinline__ bool sel_keep(int32_t x, int32_t ng, int32_t env0, int32_t nl) {
+  return MARK ? x >= 0 : in_shard(x, ng, env0, nl);
+}
+
+template <bool MARK>
 __global__ __launch_bounds__(kBlock) void shard_count_kernel(const int32_t* __restrict__ gperm,
                                                             int32_t* __restrict__ cnt, int64_t bg,
                                                             int32_t ng, int32_t env0, int32_t nl) {
@@ -123,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void shard_count_kernel(const int32_t* __re
   int32_t k = 0;
   for (int s = 0; s < kSelPer; ++s) {
     const int64_t p = c0 + (int64_t)s * kBlock + threadIdx.x;
-    if (p < bg && in_shard(src[p], ng, env0, nl)) ++k;
+    if (p < bg && sel_keep<MARK>(src[p], ng, env0, nl)) ++k;
   }
   for (int off = 32; off >= 1; off >>= 1) k += __shfl_xor(k, off);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = k;
@@ -135,6 +202,7 @@ __global__ __launch_bounds__(kBlock) void shard_count_kernel(const int32_t* __re
   }
 }
 
+template <bool MARK>
 __global__ __launch_bounds__(kBlock) void shard_write_kernel(
     const int32_t* __restrict__ gperm, const int32_t* __restrict__ cnt,
     int32_t* __restrict__ local, int32_t* __restrict__ seg, int64_t bg, int32_t ng, int32_t env0,
@@ -162,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void shard_write_kernel(
     bool keep = false;
     if (p < bg) {
       i = src[p];
-      keep = in_shard(i, ng, env0, nl);
+      keep = sel_keep<MARK>(i, ng, env0, nl);
     }
     const unsigned long long mask = __ballot(keep);
     const int32_t pre = (int32_t)__builtin_amdgcn_mbcnt_hi(
@@ -177,8 +245,12 @@ __global__ __launch_bounds__(kBlock) void shard_write_kernel(
     }
     const int32_t pos = base + wpre + pre;  // kept samples before position p in this epoch
     if (keep) {
-      const int32_t t = i / ng;
-      out[pos] = t * nl + (i - t * ng - env0);
+      if (MARK) {
+        out[pos] = i;
+      } else {
+        const int32_t t = i / ng;
+        out[pos] = t * nl + (i - t * ng - env0);
+      }
     }
     if (p < bg && p % mbg == 0) seg[e * (M + 1) + p / mbg] = pos;
     base += tot;
@@ -194,6 +266,16 @@ int fy_grid(int64_t total) {
 
 }  // namespace
 
+// DPPO_PERM_WALK: 1 = the value walk, 0 = the links + solve passes.  One GPU (the whole
+// permutation) defaults to the passes: C5's 4 x 8.4 M took 4.06-4.10 ms per learn with them
+// against 4.75-4.93 with the walk (round 5, 2 A/B reps) -- the walk's hops are dependent loads.
+// Global minibatches default to the walk: a rank walks only its 1/world of the values.
+bool perm_walk_env(bool dflt) {
+  const char* e = std::getenv("DPPO_PERM_WALK");
+  return e ? e[0] != '0' : dflt;
+}
+bool perm_walk() { return perm_walk_env(true); }
+
 int launch_perm_resolve_one(const int32_t* targets, int32_t* perms, int64_t n, int32_t* scratch,
                             hipStream_t s) {
   int32_t* head = scratch;
@@ -203,6 +285,12 @@ int launch_perm_resolve_one(const int32_t* targets, int32_t* perms, int64_t n, i
   const int G = fy_grid(n);
   DPPO_LAUNCH(fy_build_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, n, n);
   DPPO_LAUNCH_CHECK();
+  if (perm_walk_env(false)) {
+    DPPO_LAUNCH(fy_walk_scatter_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, perms, n,
+                n);
+    DPPO_LAUNCH_CHECK();
+    return DPPO_OK;
+  }
   DPPO_LAUNCH(fy_links_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, mq, perms, n, n);
   DPPO_LAUNCH_CHECK();
   DPPO_LAUNCH(fy_solve_kernel, dim3(G), dim3(kBlock), 0, s, targets, mq, perms, n, n);
@@ -235,6 +323,12 @@ int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32
   const int G = fy_grid(total);
   DPPO_LAUNCH(fy_build_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, n, total);
   DPPO_LAUNCH_CHECK();
+  if (perm_walk_env(false)) {
+    DPPO_LAUNCH(fy_walk_scatter_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, perms, n,
+                total);
+    DPPO_LAUNCH_CHECK();
+    return DPPO_OK;
+  }
   DPPO_LAUNCH(fy_links_kernel, dim3(G), dim3(kBlock), 0, s, targets, head, nxt, mq, perms, n, total);
   DPPO_LAUNCH_CHECK();
   DPPO_LAUNCH(fy_solve_kernel, dim3(G), dim3(kBlock), 0, s, targets, mq, perms, n, total);
@@ -249,10 +343,39 @@ int launch_shard_select(const int32_t* gperm, int32_t* local, int32_t* seg, int3
                         hipStream_t s) {
   if (bg <= 0 || E <= 0) return DPPO_OK;
   const dim3 grid((unsigned)shard_select_chunks(bg), (unsigned)E);
-  DPPO_LAUNCH(shard_count_kernel, grid, dim3(kBlock), 0, s, gperm, cnt, bg, ng, env0, nl);
+  DPPO_LAUNCH(shard_count_kernel<false>, grid, dim3(kBlock), 0, s, gperm, cnt, bg, ng, env0, nl);
   DPPO_LAUNCH_CHECK();
-  DPPO_LAUNCH(shard_write_kernel, grid, dim3(kBlock), 0, s, gperm, cnt, local, seg, bg, ng, env0,
-              nl, M);
+  DPPO_LAUNCH(shard_write_kernel<false>, grid, dim3(kBlock), 0, s, gperm, cnt, local, seg, bg, ng,
+              env0, nl, M);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+
+// Global minibatches from swap targets without resolving the whole permutation: this rank's
+// members of every global minibatch, in permutation order -- the same lists launch_shard_select
+// makes from the resolved permutation.  scratch: 2 * E * bg ints (bucket heads and links); marks:
+// E * bg ints.
+int launch_shard_select_targets(const int32_t* targets, int32_t* marks, int32_t* scratch,
+                                int32_t* local, int32_t* seg, int32_t* cnt, int64_t bg, int32_t ng,
+                                int32_t env0, int32_t nl, int32_t E, int32_t M, hipStream_t s) {
+  if (bg <= 0 || E <= 0) return DPPO_OK;
+  const int64_t total = bg * E;
+  int32_t* head = scratch;
+  int32_t* nxt = scratch + total;
+  DPPO_HIP_CHECK(hipMemsetAsync(head, 0xFF, (size_t)total * sizeof(int32_t), s));
+  DPPO_HIP_CHECK(hipMemsetAsync(marks, 0xFF, (size_t)total * sizeof(int32_t), s));
+  DPPO_LAUNCH(fy_build_kernel, dim3(fy_grid(total)), dim3(kBlock), 0, s, targets, head, nxt, bg,
+              total);
+  DPPO_LAUNCH_CHECK();
+  const int64_t b_local = (bg / ng) * nl;
+  DPPO_LAUNCH(fy_walk_mark_kernel, dim3(fy_grid(b_local * E)), dim3(kBlock), 0, s, targets, head,
+              nxt, marks, bg, b_local, E, ng, env0, nl);
+  DPPO_LAUNCH_CHECK();
+  const dim3 grid((unsigned)shard_select_chunks(bg), (unsigned)E);
+  DPPO_LAUNCH(shard_count_kernel<true>, grid, dim3(kBlock), 0, s, marks, cnt, bg, ng, env0, nl);
+  DPPO_LAUNCH_CHECK();
+  DPPO_LAUNCH(shard_write_kernel<true>, grid, dim3(kBlock), 0, s, marks, cnt, local, seg, bg, ng,
+              env0, nl, M);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }

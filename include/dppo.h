@@ -277,7 +277,7 @@ int dppo_perm_stats(int64_t* out3);
 /* The MT19937 half of dppo_perm_numpy: the Fisher-Yates swap targets out[c][i] = j_i
  * (i = n-1 .. 1; out[c][0] = 0) of `count` successive permutations, advancing key/pos exactly
  * as dppo_perm_numpy does.  Host only.  Draws of >= 2^22 targets run the parallel form below on
- * DPPO_PERM_PAR_THREADS threads (default 8; < 2 = serial). */
+ * DPPO_PERM_PAR_THREADS threads (default 12; < 2 = serial). */
 int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* out);
 
 /* The same draw split over `threads` threads (csrc/permpar.cpp: MT19937 jump-ahead, a
@@ -304,6 +304,17 @@ int dppo_perm_par_stats(int64_t* out3);
  * [3 * count * n].  Stream-ordered. */
 int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
                       int32_t* scratch, void* stream);
+
+/* Global minibatches on the device (dims.global_minibatches, world_size > 1): from the swap
+ * targets of the GLOBAL batch (device int32 [E][T*N*world_size], dppo_perm_targets_numpy of
+ * B*world_size), this rank's members of every global minibatch in permutation order as local
+ * sample indices (device int32 local[E][T*N]) and each epoch's minibatch boundaries (device
+ * int32 seg[E][M+1]).  Only this rank's samples are walked to their positions (the whole
+ * permutation is never resolved; DPPO_PERM_WALK=0: resolve, then select).  What
+ * dppo_learn_targets_f32 does before its minibatch steps (reference ppo.py:252-255 + the
+ * env-axis shard); exposed for drivers and for timing (class "perm").  Stream-ordered. */
+int dppo_global_minibatch_lists(dppo_handle* h, const int32_t* targets, int32_t* local,
+                                int32_t* seg, void* stream);
 
 /* Multi-GPU over RCCL (xGMI): rank 0 creates the id, the caller broadcasts it (e.g. with
  * torch.distributed), every rank attaches it to its handle.  dppo_learn_f32 then all-reduces the

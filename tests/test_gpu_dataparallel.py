@@ -45,8 +45,9 @@ def shard(host, r, Nl):
     return exp
 
 
-def run_loopback(T, Nl, D, A, cont, E, M, flat0, host, perms, global_mb):
-    """8 ranks in one loopback group; returns per-rank (params, trace)."""
+def run_loopback(T, Nl, D, A, cont, E, M, flat0, host, perms, global_mb, targets=False):
+    """8 ranks in one loopback group; returns per-rank (params, trace).  targets: `perms` holds
+    Fisher-Yates swap targets (dppo_learn_targets_f32: resolved on the device)."""
     handles = [N.Handle(0, N.Dims(T, Nl, D, A, int(cont), H, E, M, WORLD, r, int(global_mb)))
                for r in range(WORLD)]
     N.loopback_group(handles)
@@ -64,9 +65,9 @@ def run_loopback(T, Nl, D, A, cont, E, M, flat0, host, perms, global_mb):
         s = torch.cuda.Stream(device=dev())
         x = state[r]
         pr = perms if global_mb else perms[r]
-        x["rc"] = handles[r].lib.dppo_learn_f32(
-            handles[r].h, ctypes.byref(x["st"]), x["p"].data_ptr(), x["m"].data_ptr(),
-            x["v"].data_ptr(), ctypes.byref(hp), pr.ctypes.data, None, s.cuda_stream)
+        fn = handles[r].lib.dppo_learn_targets_f32 if targets else handles[r].lib.dppo_learn_f32
+        x["rc"] = fn(handles[r].h, ctypes.byref(x["st"]), x["p"].data_ptr(), x["m"].data_ptr(),
+                     x["v"].data_ptr(), ctypes.byref(hp), pr.ctypes.data, None, s.cuda_stream)
         if x["rc"] != 0:
             x["err"] = handles[r].lib.dppo_last_error()   # thread-local: read on this thread
         s.synchronize()
@@ -188,7 +189,34 @@ def test_global_minibatch_shares_are_uneven_and_exact():
     check_vs_oracle(out, params, names, L, host, perms_g, False, E, M)
 
 
-@pytest.mark.parametrize("global_mb", [False, True])
+def _perms_and_targets(n, E, seed):
+    key, pos, _ = N.mt_state(np.random.RandomState(seed))
+    perms = np.empty(E * n, np.int32)
+    N.perm_numpy(key.copy(), pos, n, E, perms)
+    tg = np.empty(E * n, np.int32)
+    N.perm_targets_numpy(key.copy(), pos, n, E, tg)
+    return perms.reshape(E, n), tg.reshape(E, n)
+
+
+@pytest.mark.parametrize("walk", ["1", "0"])
+@pytest.mark.parametrize("T,Nl,A", [(16, 32, 2), (4, 2, 3)])
+def test_world8_global_minibatches_from_swap_targets(monkeypatch, walk, T, Nl, A):
+    """Global minibatches from the device-resolved swap targets (how the engine runs them at
+    C5 sizes): with the value walk (each rank walks only its own samples to their positions,
+    DPPO_PERM_WALK=1, the default) and with the whole-permutation resolution (=0), every rank's
+    learn equals, bit for bit, the learn from the host-resolved permutations (the same members of
+    every global minibatch, in permutation order)."""
+    monkeypatch.setenv("DPPO_PERM_WALK", walk)
+    E, M, D = 4, 8, 4
+    L, names, params, flat0, host = setup(T, Nl, D, A, False, seed=9 + T)
+    perms, tg = _perms_and_targets(T * Nl * WORLD, E, seed=77 + T)
+    ref = run_loopback(T, Nl, D, A, False, E, M, flat0, host, perms, global_mb=True)
+    got = run_loopback(T, Nl, D, A, False, E, M, flat0, host, tg, global_mb=True, targets=True)
+    for r in range(WORLD):
+        assert np.array_equal(got[r][0], ref[r][0]) and np.array_equal(got[r][1], ref[r][1]), r
+
+
+@pytest.mark.parametrize("global_mb", [False, True, "targets"])
 def test_world8_c5_full_size_matches_single_gpu(global_mb):
     """BASELINE configs[4]: CartPole, 8 ranks x 8,192 envs (65,536), T = 128, mb 1,048,576
     global.  The 8-rank learn against the world-1 learn of the same 65,536-env buffer with the
@@ -197,12 +225,10 @@ def test_world8_c5_full_size_matches_single_gpu(global_mb):
     T, Nl, D, A, E, M = 128, 8192, 4, 2, 4, 8
     L, names, params, flat0, host = setup(T, Nl, D, A, False, seed=7)
     B = T * Nl
+    targets = global_mb == "targets"   # the engine's path at this size: swap targets, walked
     if global_mb:
-        key, pos, _ = N.mt_state(np.random.RandomState(42))
-        perms_g = np.empty(E * B * WORLD, np.int32)
-        N.perm_numpy(key, pos, B * WORLD, E, perms_g)
-        perms_g = perms_g.reshape(E, B * WORLD)
-        perms = perms_g
+        perms_g, tg = _perms_and_targets(B * WORLD, E, seed=42)
+        perms = tg if targets else perms_g
     else:
         perms = []
         for r in range(WORLD):
@@ -211,7 +237,8 @@ def test_world8_c5_full_size_matches_single_gpu(global_mb):
             N.perm_numpy(key, pos, B, E, pr)
             perms.append(pr.reshape(E, B))
         perms_g = union_perms(perms, T, Nl, E, M)
-    out = run_loopback(T, Nl, D, A, False, E, M, flat0, host, perms, global_mb=global_mb)
+    out = run_loopback(T, Nl, D, A, False, E, M, flat0, host, perms, global_mb=bool(global_mb),
+                       targets=targets)
     single = run_single(T, Nl * WORLD, D, A, False, E, M, flat0, host, perms_g)
     for r in range(1, WORLD):
         assert np.array_equal(out[0][0], out[r][0])

@@ -426,10 +426,13 @@ def test_indivisible_minibatch_raises_value_error():
         agent.learn(exp)
 
 
+@pytest.mark.parametrize("walk", ["1", "0"])
 @pytest.mark.parametrize("n,count", [(1, 1), (2, 3), (3, 4), (17, 2), (1000, 4), (65539, 2),
                                      (524288, 4)])
-def test_device_fisher_yates_resolution_matches_numpy(n, count):
-    """dppo_perm_resolve(host MT19937 targets) == np.random.permutation, bit-exact."""
+def test_device_fisher_yates_resolution_matches_numpy(monkeypatch, walk, n, count):
+    """dppo_perm_resolve(host MT19937 targets) == np.random.permutation, bit-exact: by the value
+    walk (DPPO_PERM_WALK=1, default) and by the links + chain passes (=0)."""
+    monkeypatch.setenv("DPPO_PERM_WALK", walk)
     np.random.seed(1000 + n)
     key, pos, _ = N.mt_state()
     tg = np.empty(count * n, np.int32)

@@ -106,17 +106,17 @@ def test_peer_exchange_drop_in_agent(tmp_path):
     assert np.array_equal(r0["trace"], r1["trace"])
 
 
-@pytest.mark.parametrize("variant", ["coarse", "fine", "wrap"])
+@pytest.mark.parametrize("variant", ["uncached", "coarse", "fine", "wrap"])
 def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(monkeypatch, variant):
     """A 1-rank peer exchange in this process: every learn() then takes the multi-rank sequence
     of a node with one GPU per rank -- the advantage statistics through the exchange kernel, and
     each minibatch's gradient exchange INSIDE reduce_adam_kernel (publish the block's slice, wait
     for every rank's flag, sum in rank order) -- and must reproduce the reference's captured
     traces.  (Two ranks sharing this GPU take the unfused exchange: their optimizer-step grids
-    could not be resident at once; the test above.)  Variants: the exchange buffer fine-grained,
-    and the fused exchange counting on from just below the 2^32 sequence wrap (test hook)."""
-    if variant == "fine":
-        monkeypatch.setenv("DPPO_PEER_MEM", "fine")
+    could not be resident at once; the test above.)  Variants: the exchange buffer uncached (the
+    default), coarse- or fine-grained, and the fused exchange counting on from just below the 2^32 sequence wrap (test hook)."""
+    if variant in ("coarse", "fine"):
+        monkeypatch.setenv("DPPO_PEER_MEM", variant)
     if variant == "wrap":
         monkeypatch.setenv("DPPO_TEST_HOOKS", "1")
         monkeypatch.setenv("DPPO_PEER_XSEQ0", str(0xFFFFFFF0))
@@ -134,7 +134,8 @@ def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(monkeypat
         assert not h.peer_selftest(stream())
         info = h.peer_info()
         assert info["ranks"] == 1 and info["fused"], info
-        assert info["memory"] == ("fine-grained" if variant == "fine" else "coarse-grained")
+        assert info["memory"] == {"coarse": "coarse-grained", "fine": "fine-grained"}.get(
+            variant, "uncached")
         seq0 = info["exchanges"]
         h.set_timing(True)
         losses, norms = [], []

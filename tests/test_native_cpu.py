@@ -261,6 +261,43 @@ def closed_form_shuffle(j):
     return out
 
 
+def value_walk_positions(j):
+    """NumPy restatement of the device value walk (csrc/shuffle.hip walk_pos): value v starts at
+    position q = v; the largest step i in (q, bound) with j[i] = q moves it up to i (final),
+    otherwise step q moves it down to j[q] (j[q] = q: final) and bound becomes q."""
+    n = len(j)
+    buckets = {}
+    for i in range(1, n):
+        buckets.setdefault(int(j[i]), []).append(i)
+    pos = np.empty(n, np.int64)
+    for v in range(n):
+        q, bound = v, n
+        while True:
+            best = max([i for i in buckets.get(q, []) if q < i < bound], default=-1)
+            if best >= 0 or q == 0:
+                pos[v] = max(best, 0)
+                break
+            if j[q] == q:
+                pos[v] = q
+                break
+            bound, q = q, int(j[q])
+    return pos
+
+
+def test_value_walk_is_the_inverse_shuffle():
+    """Every value walks to the position the sequential Fisher-Yates loop puts it at: all-zero,
+    identity, shifted and random targets."""
+    rng = np.random.default_rng(4)
+    for n in (1, 2, 5, 64, 300):
+        cases = [np.zeros(n, np.int64), np.arange(n), np.maximum(np.arange(n) - 1, 0),
+                 np.array([0] + [rng.integers(0, i + 1) for i in range(1, n)])]
+        for j in cases:
+            a = fisher_yates(j)
+            inv = np.empty(n, np.int64)
+            inv[a] = np.arange(n)
+            assert np.array_equal(value_walk_positions(j), inv)
+
+
 def test_closed_form_shuffle_on_adversarial_targets():
     """All-zero, identity and random targets (every j_i <= i is a valid Fisher-Yates input)."""
     rng = np.random.default_rng(3)

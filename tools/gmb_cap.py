@@ -8,8 +8,9 @@ For world = 1, 2, 4, 8:
 * host draw per learn: the serial accept scan (perm.cpp) and the parallel speculative draw
   (permpar.cpp, DPPO_PERM_PAR_THREADS threads; what dppo_perm_targets_numpy runs), median of 5;
 * on a GPU box: the device time per learn of one rank's share (T x 65,536/world envs, local
-  minibatches, the same kernels) plus the device work every rank repeats in global mode -- the
-  Fisher-Yates resolution of all E x 8.4 M targets (the "perm" kernels of the one-GPU C5 learn).
+  minibatches, the same kernels) plus that rank's global-minibatch member lists from the swap
+  targets (dppo_global_minibatch_lists: bucket build over all E x 8.4 M targets, the walk of the
+  rank's own samples, the ordered selection); at world 1 the whole-permutation resolution.
 The look-ahead drafts overlap the draw with the device, so a learn takes
 max(draw, share + resolution); the cap is device(1) / that.
 
@@ -42,6 +43,37 @@ def host_draw_ms(n, epochs=4, reps=5, threads=1):
     return float(np.median(ts))
 
 
+def global_lists_ms(world, reps=5):
+    """Device time of one rank's global-minibatch member lists at configs[4] over `world` ranks
+    (dppo_global_minibatch_lists: bucket build over all 4 x 8.4 M targets, the walk of this
+    rank's 1/world of the samples, the ordered selection), HIP events on the kernels."""
+    import torch
+    from diamond import _native as N
+    T, Ng, E, M = 128, 65536, 4, 8
+    Nl = Ng // world
+    h = N.Handle(0, N.Dims(T, Nl, 4, 2, 0, 64, E, M, world, 0, 1))
+    key, pos, _ = N.mt_state(np.random.RandomState(7))
+    tg = np.empty(E * T * Ng, np.int32)
+    N.perm_targets_numpy(key, pos, T * Ng, E, tg)
+    dev = torch.device("cuda", 0)
+    td = torch.from_numpy(tg).to(dev)
+    local = torch.empty(E * T * Nl, dtype=torch.int32, device=dev)
+    seg = torch.empty(E * (M + 1), dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    call = lambda: N.check(h.lib.dppo_global_minibatch_lists(h.h, td.data_ptr(), local.data_ptr(),
+                                                             seg.data_ptr(), s),
+                           "dppo_global_minibatch_lists")
+    call()
+    torch.cuda.synchronize(dev)
+    h.set_timing(True)
+    for _ in range(reps):
+        call()
+    ms, cnt = h.timing()["perm"]
+    h.set_timing(False)
+    h.close()
+    return ms / cnt
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--no-gpu", action="store_true")
@@ -49,7 +81,7 @@ def main():
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     T, Ng = 128, 65536
-    threads = int(os.environ.get("DPPO_PERM_PAR_THREADS", "8"))
+    threads = int(os.environ.get("DPPO_PERM_PAR_THREADS", "12"))
     draw_serial = host_draw_ms(T * Ng)
     draw_par = host_draw_ms(T * Ng, threads=threads)
     dev, resolve = {}, None
@@ -65,18 +97,19 @@ def main():
             dev[world] = r["device_ms_per_step"]
             if world == 1:  # the one-GPU learn resolves all 4 x 8.4 M targets on the device
                 k = r["kernels"].get("perm")
-                resolve = k["ms_total"] / a.steps if k else None
-                dev[1] = r["device_ms_per_step"]
+                resolve = {1: k["ms_total"] / a.steps if k else 0.0}
+        for world in (2, 4, 8):
+            resolve[world] = global_lists_ms(world)
     rows = []
     for world in (1, 2, 4, 8):
         row = {"world": world, "host_draw_ms_serial": round(draw_serial, 2),
                "host_draw_ms_parallel": round(draw_par, 2), "draw_threads": threads,
                "global_samples": T * Ng, "targets_drawn": 4 * T * Ng}
         if dev:
-            share = dev[world] - (resolve if world == 1 else 0.0)
-            rdev = share + (resolve or 0.0)  # every rank resolves the global permutations
+            share = dev[world] - (resolve[1] if world == 1 else 0.0)
+            rdev = share + resolve[world]  # each rank: its share + its global member lists
             row["device_ms_share_local"] = round(share, 3)
-            row["device_ms_resolution"] = round(resolve or 0.0, 3)
+            row["device_ms_global_lists"] = round(resolve[world], 3)
             row["device_ms_per_learn_global"] = round(rdev, 3)
             for tag, draw in (("serial", draw_serial), ("parallel", draw_par)):
                 bound = max(draw, rdev)

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--threads", default="4,8,12,16")
+    ap.add_argument("--chunks-per-thread", type=int, default=0,
+                    help="chunks = this x threads (0: the library default, 2 per thread)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from diamond import _native as N
@@ -58,11 +60,12 @@ def main():
         states.append((key, pos, k1, p1, r1))
     for thr in by_thr:
         key, pos = states[0][0], states[0][1]
-        N.perm_targets_numpy_par(key.copy(), pos, n, E, got, thr)  # warm-up
+        ch = a.chunks_per_thread * thr
+        N.perm_targets_numpy_par(key.copy(), pos, n, E, got, thr, chunks=ch)  # warm-up
         for rep, (key, pos, k1, p1, r1) in enumerate(states):
             k2 = key.copy()
             t0 = time.perf_counter()
-            p2, st = N.perm_targets_numpy_par(k2, pos, n, E, got, thr)
+            p2, st = N.perm_targets_numpy_par(k2, pos, n, E, got, thr, chunks=ch)
             ms = (time.perf_counter() - t0) * 1e3
             ok = bool(p1 == p2 and np.array_equal(k1, k2) and np.array_equal(r1, got))
             by_thr[thr].append(ms)
