@@ -408,6 +408,7 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "scaling": scaling,
         "config": {"workload": f"{model}: learn() = old-policy eval + GAE + adv-norm + "
                                f"{E}x{M} minibatch Adam steps", "name": name,
+                   "baseline_config": BASELINE_INDEX.get(name),
                    "rollout_steps": T, "num_envs_per_gpu": N, "num_envs_total": N * world,
                    "obs_dim": D, "act_dim": A, "continuous": cont, "hidden": H,
                    "batch_per_learn": B_global, "minibatch": B_global // M,
@@ -538,6 +539,11 @@ def spawn_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+# bench config name -> its entry in BASELINE.json "configs"
+BASELINE_INDEX = {"cartpole4096": "configs[1]", "lunar8192": "configs[2]",
+                  "cheetah4096": "configs[3]", "c5": "configs[4]"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -642,6 +648,17 @@ def main():
             extra[name]["roofline"] = r["roofline"]
             extra[name]["config"] = r["config"]
         out["configs_extra"] = extra
+    if rank == 0 and world == 1:
+        # The headline workload moved in round 4 from configs[1] (CartPole, 4,096 envs; rounds
+        # 1-3) to configs[2] (LunarLander, 8,192 envs: the largest one-GPU config and the north
+        # star's GAE size); lines of different rounds compare by this key, and the configs[1]
+        # number stays beside it (configs_extra.cartpole4096)
+        c1 = out.get("configs_extra", {}).get("cartpole4096", {}).get("value")
+        if args.config == "cartpole4096":
+            c1 = out["value"]
+        out["headline"] = {"name": args.config, "baseline_config": BASELINE_INDEX.get(args.config),
+                           "since": "round 4 (rounds 1-3: configs[1] cartpole4096)",
+                           "configs1_cartpole4096_value": c1}
     if rank == 0 and world == 1 and not args.no_gae_roofline:
         out["roofline_gae"] = gae_roofline(device)
         out["roofline_gae_affine"] = gae_roofline(device, mode=1)

@@ -483,6 +483,7 @@ struct Chunk {
   bool overflow = false;
   double us = 0, jump_us = 0;
   int64_t scalar_words = 0;
+  uint64_t twist_tsc = 0, scan_tsc = 0;  // DPPO_PAR_DBG_CHUNKS: time stamp counts
   // outputs of the stitch
   std::vector<Op> ops;
   std::vector<int32_t> lits;
@@ -649,13 +650,16 @@ PAR_AVX512 void scan_chunk(const Draw& D, Chunk& C, bool last, int64_t est_targe
   int64_t ns = 0;  // guessed targets stored
   int64_t scap = (int64_t)C.S.size() - 32;
   uint32_t q = 0;
-  const __m512i lane = _mm512_set_epi32(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
-  (void)lane;
+  static const bool dbg_tsc = std::getenv("DPPO_PAR_DBG_CHUNKS") != nullptr;
+  C.twist_tsc = 0;
+  const uint64_t ts0 = dbg_tsc ? __rdtsc() : 0;
   for (;;) {
     if (!last && (int64_t)q >= C.len) break;
     if (last && r.k >= stop_k) break;
     if (opos == kN) {
+      const uint64_t tt0 = dbg_tsc ? __rdtsc() : 0;
       twist_temper(mt, out);
+      if (dbg_tsc) C.twist_tsc += __rdtsc() - tt0;
       ++blk;
       opos = 0;
       if (r.k >= key_from) {
@@ -663,10 +667,76 @@ PAR_AVX512 void scan_chunk(const Draw& D, Chunk& C, bool last, int64_t est_targe
         C.keys.insert(C.keys.end(), mt, mt + kN);
       }
     }
-    if (ns + 16 > scap) {
+    if (ns + 64 > scap) {
       C.S.resize(C.S.size() * 3 / 2 + 65536);
       S = C.S.data();
       scap = (int64_t)C.S.size() - 32;
+    }
+    // ---- 64 words at once: one threshold pair for the whole group (every v <= i - 63 is
+    // accepted and every v > i rejected whatever the others do), so the loop-carried chain
+    // (threshold -> compare -> popcount -> i) runs once per 64 words instead of per 16; a group
+    // with a word in (i - 63, i] falls through to the 16-word step
+    if (!r.done && opos + 64 <= kN && (last || (int64_t)q + 64 <= C.len) &&
+        r.i >= r.lo + 63 && r.k + 64 < toggle && r.k + 64 < D.K) {
+      const uint32_t ii = r.i;
+      const __m512i vm = _mm512_set1_epi32((int)r.mask);
+      const __m512i ta = _mm512_set1_epi32((int)(ii - 63));
+      const __m512i tl = _mm512_set1_epi32((int)ii);
+      __m512i v[4];
+      __mmask16 a16[4];
+      uint64_t acc = 0, le = 0;
+      for (int g = 0; g < 4; ++g) {
+        v[g] = _mm512_and_si512(_mm512_loadu_si512((const void*)(out + opos + 16 * g)), vm);
+        a16[g] = _mm512_cmple_epu32_mask(v[g], ta);
+        acc |= (uint64_t)a16[g] << (16 * g);
+        le |= (uint64_t)_mm512_cmple_epu32_mask(v[g], tl) << (16 * g);
+      }
+      if (!(le & ~acc)) {
+        if (W >= 0) {
+          // near misses: u = v - i_l in [-W + 1, W] needs v in (ii - 63 - W, ii + W]
+          const __m512i nlo = _mm512_set1_epi32((int)std::max<int64_t>((int64_t)ii - 63 - W, -1));
+          const __m512i nhi = _mm512_set1_epi32((int)std::min<int64_t>((int64_t)ii + W, 0x7FFFFFFF));
+          uint64_t near = 0;
+          for (int g = 0; g < 4; ++g)
+            near |= (uint64_t)(_mm512_cmpgt_epi32_mask(v[g], nlo) &
+                               _mm512_cmple_epi32_mask(v[g], nhi)) << (16 * g);
+          if (near) {
+            alignas(64) uint32_t vl[64];
+            for (int g = 0; g < 4; ++g) _mm512_store_si512((void*)(vl + 16 * g), v[g]);
+            const int64_t s0 = r.k - C.kg0;
+            for (uint64_t nm = near; nm; nm &= nm - 1) {
+              const int l = __builtin_ctzll(nm);
+              const int before = __builtin_popcountll(acc & ((1ull << l) - 1));
+              const int64_t u = (int64_t)vl[l] - ((int64_t)ii - before);
+              if (u <= W && u >= -W) record(q + (uint32_t)l, s0 + before, u, vl[l]);
+            }
+          }
+        }
+        for (int g = 0; g < 4; ++g) {
+          _mm512_storeu_si512((void*)(S + ns), _mm512_maskz_compress_epi32(a16[g], v[g]));
+          ns += __builtin_popcount((unsigned)a16[g]);
+        }
+        if (zone) {
+          raw_room(64);
+          for (int g = 0; g < 4; ++g)
+            _mm512_storeu_si512((void*)(C.raw.data() + C.nraw + 16 * g),
+                                _mm512_loadu_si512((const void*)(out + opos + 16 * g)));
+          const int sh = (int)(C.nraw & 63);
+          C.bits[(size_t)(C.nraw >> 6)] |= acc << sh;
+          if (sh) C.bits[(size_t)(C.nraw >> 6) + 1] |= acc >> (64 - sh);
+          C.nraw += 64;
+        }
+        const int cnt = __builtin_popcountll(acc);
+        q += 64;
+        opos += 64;
+        r.k += cnt;
+        r.i -= (uint32_t)cnt;
+        if (r.i < r.lo) {  // one band down (i >= lo - 1 >= 1 here)
+          r.mask = smear(r.i);
+          r.lo = (r.mask >> 1) + 1;
+        }
+        continue;
+      }
     }
     // ---- 16 words at once
     if (!r.done && opos + 16 <= kN && (last || (int64_t)q + 16 <= C.len) &&
@@ -748,6 +818,7 @@ PAR_AVX512 void scan_chunk(const Draw& D, Chunk& C, bool last, int64_t est_targe
     }
   }
   if (zone) C.zones.back().q1 = q;
+  if (dbg_tsc) C.scan_tsc = __rdtsc() - ts0;
   C.words = q;
   C.scalar_words = scalar_words;
   C.kg_end = r.k;
@@ -1495,6 +1566,15 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
     gen += ch.words;
     scan_max = std::max(scan_max, ch.us);
   }
+  if (std::getenv("DPPO_PAR_DBG_CHUNKS"))
+    for (const Chunk& ch : D.ch)
+      std::fprintf(stderr,
+                   "chunk words %lld us %.0f jump %.0f recs %zu raw %lld scalar %lld W %lld "
+                   "tsc/word: loop %.2f twist %.2f\n",
+                   (long long)ch.words, ch.us, ch.jump_us, ch.rq.size(), (long long)ch.nraw,
+                   (long long)ch.scalar_words, (long long)ch.W,
+                   (double)ch.scan_tsc / (double)std::max<int64_t>(ch.words, 1),
+                   (double)ch.twist_tsc / (double)std::max<int64_t>(ch.words, 1));
   if (st) {
     st[1] = C;
     st[2] = recs;

@@ -216,3 +216,17 @@ def test_bench_gpus_flag_starts_the_ranks_itself():
         assert mg["c5_update_steps_speedup_vs_world1"][m] > 0
     assert mg["c5_strong_global"]["perm_device_ms_per_step"] > 0
     assert mg["c5_world1_anchor"]["update_steps_per_s"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_one_gpu_line_names_its_baseline_config():
+    """The N = 1 line (the driver's BENCH line) names which BASELINE config its headline is --
+    configs[2] since round 4 -- and carries the roofline of its dominant kernel."""
+    import sys
+    d = _bench_line([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--no-extra",
+                     "--no-cpu-baseline", "--no-gae-roofline"])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["unit"] == "env-steps/s"
+    assert d["config"]["baseline_config"] == "configs[2]"
+    assert d["headline"]["name"] == "lunar8192" and d["headline"]["baseline_config"] == "configs[2]"
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and 0 < r["frac"] < 1 and r["unit"] == "TFLOP/s"
