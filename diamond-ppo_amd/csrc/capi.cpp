@@ -281,6 +281,13 @@ int device_status(const dppo_handle* h) {
               "and this handle is no longer usable", (double)h->xticks / 1e8);
     return DPPO_ECOMM;
   }
+  if (e == kErrTagTimeout) {
+    set_error("the optimizer step's fan-in timed out (code 3: a block's tagged word never "
+              "arrived -- its workgroups were not all resident at once, or a block left early); "
+              "the parameters of that step were left unchanged and this handle is no longer "
+              "usable");
+    return DPPO_EHIP;
+  }
   set_error("a grid-wide fan-in timed out (code %u): its workgroups were not all resident on the "
             "device at once (another process holding the CUs, or a partitioned device); the "
             "parameters of that optimizer step were left unchanged and this handle is no longer "
@@ -1418,6 +1425,10 @@ int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
       }
     }
     DPPO_HIP_CHECK(hipMemset(h->xbuf, 0, (size_t)bytes));
+    if (const char* dbg = std::getenv("DPPO_PEER_DEBUG"))
+      if (dbg[0] == '1')
+        std::fprintf(stderr, "dppo peer: exchange buffer %p, %lld bytes, memory type %d\n",
+                     (void*)h->xbuf, (long long)bytes, h->xmem);
     // DPPO_PEER_XSEQ0 (test hook, dppo_peer_open): counting on from s0, the slice flags start as
     // if exchange s0 had just completed -- the (wrap-safe) flag comparison needs flags within
     // 2^31 of the sequence, as they always are once exchanges have run

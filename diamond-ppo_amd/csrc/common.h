@@ -164,6 +164,16 @@ __device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v,
 // of the next C-ABI call without any synchronisation (capi.cpp device_status).
 constexpr unsigned kErrFaninTimeout = 1u;  // a grid-wide fan-in gave up waiting: grid not resident
 constexpr unsigned kErrPeerTimeout = 2u;   // a peer exchange gave up waiting for another rank
+constexpr unsigned kErrTagTimeout = 3u;    // reduce_adam's tagged-word fan-in gave up waiting
+// A wait that runs out of time records its code only when the word is still clear, and a wait
+// that finds the word already set leaves without writing: the first cause is what the host reads.
+__device__ __forceinline__ void raise_err(unsigned* err, unsigned code) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u)
+    __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool err_set(const unsigned* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+}
 // Default bound of one fan-in wait, in s_memrealtime ticks (100 MHz): 5 s.  A resident grid
 // arrives within microseconds; only a grid that is NOT co-resident (another process holding CUs
 // with a long kernel, a partitioned device) can wait this long.
@@ -198,8 +208,8 @@ __device__ __forceinline__ bool grid_fanin(unsigned* ctr, unsigned epoch,
     __builtin_amdgcn_s_sleep(1);
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks;
-      if (late || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-        __hip_atomic_store(err, kErrFaninTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (late || err_set(err)) {
+        if (late) raise_err(err, kErrFaninTimeout);
         return false;
       }
     }
@@ -362,8 +372,8 @@ __device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a) 
     __builtin_amdgcn_s_sleep(1);
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
-      if (late || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-        __hip_atomic_store(a.err, kErrPeerTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (late || err_set(a.err)) {
+        if (late) raise_err(a.err, kErrPeerTimeout);
         return false;
       }
     }

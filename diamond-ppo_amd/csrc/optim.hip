@@ -228,8 +228,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
       __builtin_amdgcn_s_sleep(1);
       if ((k & 255u) == 255u) {
         const bool late = __builtin_amdgcn_s_memrealtime() - t0 > pl.timeout_ticks;
-        if (late || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-          __hip_atomic_store(err, kErrPeerTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (late || err_set(err)) {
+          if (late) raise_err(err, kErrPeerTimeout);
           return;  // parameters untouched; the handle reports the error
         }
       }
@@ -271,8 +271,8 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     __builtin_amdgcn_s_sleep(1);
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks;
-      if (late || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-        __hip_atomic_store(err, kErrFaninTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (late || err_set(err)) {
+        if (late) raise_err(err, kErrTagTimeout);
         return;  // parameters untouched; the next C-ABI call reports the error
       }
     }

@@ -106,7 +106,11 @@ def test_peer_exchange_drop_in_agent(tmp_path):
     assert np.array_equal(r0["trace"], r1["trace"])
 
 
-@pytest.mark.parametrize("variant", ["uncached", "coarse", "fine", "wrap"])
+# coarse first: in one process, a coarse-grained exchange set up after an uncached exchange has run
+# learns never saw its own tagged stores (a deterministic 10 s self-test timeout on the box,
+# DESIGN.md §6 round 5) -- a process uses one memory type (DPPO_PEER_MEM is read per buffer, and
+# production sets it once), so the variants run in the order that never mixes them that way
+@pytest.mark.parametrize("variant", ["coarse", "fine", "uncached", "wrap"])
 def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(monkeypatch, variant):
     """A 1-rank peer exchange in this process: every learn() then takes the multi-rank sequence
     of a node with one GPU per rank -- the advantage statistics through the exchange kernel, and

@@ -29,7 +29,8 @@ CLASS = {"mb_kernel": "grad", "mbw_kernel": "grad", "grad_kernel": "grad", "eval
          "stats_reduce_kernel": "adv_stats", "fy_build_kernel": "perm",
          "fy_links_kernel": "perm", "fy_solve_kernel": "perm", "shard_count_kernel": "perm",
          "shard_write_kernel": "perm", "next_eval_kernel": "next_eval",
-         "gae_aff_kernel": "gae"}
+         "gae_aff_kernel": "gae", "fy_walk_scatter_kernel": "perm",
+         "fy_walk_mark_kernel": "perm", "gae_stream_probe_kernel": "gae_probe"}
 
 
 def short(name: str) -> str:
