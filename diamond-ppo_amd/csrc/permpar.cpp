@@ -34,6 +34,7 @@
 // serial draw, so the result is always exact; dppo_perm_targets_numpy_par reports which path ran.
 #include <immintrin.h>
 #include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -41,6 +42,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -1345,8 +1347,70 @@ class Pool {
     while ((int)workers_.size() < nw) {
       const int id = (int)workers_.size();
       workers_.emplace_back([this, id] { loop(id); });
+      // Helper k runs on a physical core of its own (one logical CPU per core of the affinity
+      // mask; DPPO_PERM_PAR_PIN=0 leaves placement to the scheduler).  Left to the scheduler on
+      // the box's shared 256-CPU host, helpers landed on busy or sibling CPUs: the MT19937 twist
+      // -- pure L1 compute -- ran 0.66 TSC ticks per word at the median instead of 0.36, and a
+      // chained draw took 7.0-7.4 ms instead of 5.0-5.4 at 12 threads (tools/gpu/r05_draw_pin.sh).
+      const char* e = std::getenv("DPPO_PERM_PAR_PIN");
+      if (!(e && e[0] == '0')) {
+        const std::vector<int>& cores = pin_cores();
+        if (!cores.empty()) {
+          cpu_set_t set;
+          CPU_ZERO(&set);
+          CPU_SET(cores[(size_t)(pin_base() + id + 1) % cores.size()], &set);
+          pthread_setaffinity_np(workers_.back().native_handle(), sizeof(set), &set);
+        }
+      }
       workers_.back().detach();
     }
+  }
+  // Where this process's block of helper cores starts in pin_cores(): with several ranks per
+  // node (torchrun's LOCAL_RANK / LOCAL_WORLD_SIZE), rank r takes the cores r x (threads + 1)
+  // on, so that the ranks' helpers never share a core; one process starts at the caller's core.
+  static size_t pin_base() {
+    const char* lr = std::getenv("LOCAL_RANK");
+    const char* lw = std::getenv("LOCAL_WORLD_SIZE");
+    if (!lr || !lw || std::atoi(lw) <= 1) return 0;
+    const char* t = std::getenv("DPPO_PERM_PAR_THREADS");
+    const int per = (t ? std::max(1, std::atoi(t)) : 12) + 1;
+    return (size_t)std::max(0, std::atoi(lr)) * (size_t)per;
+  }
+  // one logical CPU per physical core of the affinity mask (in mask order; one process: rotated
+  // to start at the caller's core)
+  static const std::vector<int>& pin_cores() {
+    static const std::vector<int> v = [] {
+      std::vector<int> out;
+      cpu_set_t m;
+      if (sched_getaffinity(0, sizeof(m), &m) != 0) return out;
+      std::vector<int> all;
+      for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &m)) all.push_back(c);
+      std::vector<bool> taken(CPU_SETSIZE, false);
+      for (int c : all) {
+        if (taken[(size_t)c]) continue;
+        out.push_back(c);
+        char path[96];
+        std::snprintf(path, sizeof(path),
+                      "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c);
+        if (FILE* f = std::fopen(path, "r")) {
+          int a = -1, b = -1;
+          char sep = 0;
+          if (std::fscanf(f, "%d%c%d", &a, &sep, &b) >= 1) {
+            if (a >= 0 && a < CPU_SETSIZE) taken[(size_t)a] = true;
+            if (b >= 0 && b < CPU_SETSIZE) taken[(size_t)b] = true;
+          }
+          std::fclose(f);
+        }
+      }
+      if (pin_base() == 0) {
+        const int me = sched_getcpu();
+        auto it = std::find(out.begin(), out.end(), me);
+        if (it != out.end()) std::rotate(out.begin(), it, out.end());
+      }
+      return out;
+    }();
+    return v;
   }
   void loop(int id) {
     uint64_t seen = 0;

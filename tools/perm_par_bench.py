@@ -3,8 +3,11 @@
 minibatches (E = 4 permutations of T x 65,536 = 8,388,608 samples: ppo.py:252-255), serial
 (perm.cpp) against the parallel speculative draw (permpar.cpp) at several thread counts.
 Every parallel draw is checked bit for bit (targets, MT19937 key and pos) against the serial one.
+--chain K also times K draws back to back, each from the previous one's final state (what the
+learner's look-ahead drafts do when the draw is the bound: no idle time between draws, so the
+helper threads' cores stay busy), the last one checked against K chained serial draws.
 
-    python tools/perm_par_bench.py [--reps 5] [--threads 4,8,12,16] [--out file.json]
+    python tools/perm_par_bench.py [--reps 5] [--threads 4,8,12,16] [--chain 8] [--out file.json]
 """
 import argparse
 import json
@@ -36,6 +39,7 @@ def main():
     ap.add_argument("--threads", default="4,8,12,16")
     ap.add_argument("--chunks-per-thread", type=int, default=0,
                     help="chunks = this x threads (0: the library default, 2 per thread)")
+    ap.add_argument("--chain", type=int, default=0)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from diamond import _native as N
@@ -74,6 +78,26 @@ def main():
             print(json.dumps(st), flush=True)
             if not ok:
                 raise SystemExit(f"MISMATCH at threads={thr} rep={rep}")
+    chained = {}
+    if a.chain > 0:
+        key0, pos0 = states[0][0], states[0][1]
+        kc, pc = key0.copy(), pos0
+        ref = np.empty(n * E, np.int32)
+        for _ in range(a.chain):
+            pc, _ = N.perm_targets_numpy_par(kc, pc, n, E, ref, 1)
+        for thr in by_thr:
+            ch = a.chunks_per_thread * thr
+            kk, pp = key0.copy(), pos0
+            ts = []
+            for _ in range(a.chain):
+                t0 = time.perf_counter()
+                pp, _ = N.perm_targets_numpy_par(kk, pp, n, E, got, thr, chunks=ch)
+                ts.append((time.perf_counter() - t0) * 1e3)
+            ok = bool(pp == pc and np.array_equal(kk, kc) and np.array_equal(got, ref))
+            if not ok:
+                raise SystemExit(f"chained MISMATCH at threads={thr}")
+            chained[thr] = [round(t, 3) for t in ts]
+            print(json.dumps({"threads": thr, "chained_ms": chained[thr]}), flush=True)
     med = lambda x: round(float(np.median(x)), 3)
     summary = {"cpu": cpu_model(), "affinity_cpus": len(os.sched_getaffinity(0)),
                "n": n, "epochs": E, "targets": E * (n - 1),
@@ -82,6 +106,9 @@ def main():
                "parallel_ms_min": {t: round(min(v), 3) for t, v in by_thr.items()},
                "fallbacks": sum(1 for r in rows if r["path"] != 1),
                "all_bit_exact": all(r["bit_exact"] for r in rows)}
+    if chained:
+        summary["chained_ms_median"] = {t: med(v[1:]) for t, v in chained.items()}
+        summary["chained_ms_min"] = {t: round(min(v[1:]), 3) for t, v in chained.items()}
     print(json.dumps(summary), flush=True)
     if a.out:
         with open(a.out, "w") as f:
