@@ -494,6 +494,7 @@ struct Chunk {
 
 struct Draw {
   int64_t n = 0, K = 0;
+  double inv_n1 = 0;  // 1 / (n - 1)
   int32_t count = 0;
   int P0 = 0;
   const uint32_t* key0 = nullptr;
@@ -516,7 +517,11 @@ struct Draw {
 
   int band(int64_t k) const {  // band id of counter k (-1: the draw is done)
     if (k >= K) return -1;
-    const int64_t e = k / (n - 1);
+    // the epoch k / (n - 1) by a double reciprocal, corrected by one step either way (the
+    // stitch calls this per replayed word; a 64-bit division was its largest single cost)
+    int64_t e = (int64_t)((double)k * inv_n1);
+    if (e * (n - 1) > k) --e;
+    else if ((e + 1) * (n - 1) <= k) ++e;
     const uint32_t i = (uint32_t)(n - 1 - (k - e * (n - 1)));
     return (int)(e * 64 + (31 - __builtin_clz(i)));
   }
@@ -843,6 +848,7 @@ struct Stitch {
   const Draw& D;
   explicit Stitch(const Draw& d) : D(d) {}
   int64_t exact_words = 0, max_delta = 0, triggers = 0;
+  double wait_us = 0;     // time spent waiting for chunk scans (stats: the stitch's own work)
   int fail = 0;           // reason code of a failed stitch
   int64_t end_word = -1;  // global index of the word after the last accepted one
 
@@ -975,9 +981,24 @@ PAR_AVX512 bool stitch_all(Draw& D, Stitch& X) {
   enum { OFFSET, EXACT, LOCKED } mode = OFFSET;
   int64_t kt = 0;
   for (size_t c = 0; c < D.ch.size(); ++c) {
-    D.wait_scanned(c);
+    {
+      const auto w0 = std::chrono::steady_clock::now();
+      D.wait_scanned(c);
+      X.wait_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - w0)
+                       .count();
+    }
     if (c > 0) D.mark_stitched(c - 1, c);  // chunk c-1's ops are final
     Chunk& C = D.ch[c];
+    // every disagreement is a record (~1/6 of them disagree in practice) and costs at most two
+    // ops and a literal; the replayed zone words add literals: reserved up front from those
+    // counts, so the vectors rarely grow inside the serial stitch (growing them there cost ~3x
+    // per trigger in the draws that outgrew the previous capacity)
+    {
+      const size_t nops = C.rq.size() + (size_t)C.zones.size() * 64 + 1024;
+      const size_t nlits = C.rq.size() + (size_t)C.nraw + 1024;
+      if (C.ops.capacity() < nops) C.ops.reserve(nops);
+      if (C.lits.capacity() < nlits) C.lits.reserve(nlits);
+    }
     X.C = &C;
     X.kt = kt;
     X.s = 0;
@@ -1356,9 +1377,12 @@ class Pool {
       if (!(e && e[0] == '0')) {
         const std::vector<int>& cores = pin_cores();
         if (!cores.empty()) {
+          // DPPO_PERM_PAR_PIN=2 (A/B): the block taken from the far end of the list
+          const size_t k = (pin_base() + id + 1) % cores.size();
+          const size_t at = (e && e[0] == '2') ? cores.size() - 1 - k : k;
           cpu_set_t set;
           CPU_ZERO(&set);
-          CPU_SET(cores[(size_t)(pin_base() + id + 1) % cores.size()], &set);
+          CPU_SET(cores[at], &set);
           pthread_setaffinity_np(workers_.back().native_handle(), sizeof(set), &set);
         }
       }
@@ -1472,6 +1496,7 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
   const double t_start = now_us();
   Draw D;
   D.n = n;
+  D.inv_n1 = n > 1 ? 1.0 / (double)(n - 1) : 0.0;
   D.count = count;
   D.K = (int64_t)count * (n - 1);
   D.P0 = *pos;
@@ -1655,6 +1680,7 @@ bool par_draw(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* ou
     st[15] = (int64_t)jump_max;
     st[16] = scal;
     st[17] = X.triggers;
+    st[18] = (int64_t)(t3 - t1 - X.wait_us);  // the stitch's own work (its waits excluded)
   }
   if (!ok) return false;
   // the generator state after the last consumed word

@@ -250,7 +250,7 @@ def perm_targets_numpy(key: np.ndarray, pos: int, n: int, count: int,
 
 PAR_STATS = ["path", "chunks", "records", "zone_words", "replayed_words", "max_offset", "W", "Wb",
              "scan_us", "stitch_us", "assembly_us", "slowest_chunk_us", "words", "fail", "total_us",
-             "jump_us", "scalar_words", "triggers"]
+             "jump_us", "scalar_words", "triggers", "stitch_work_us"]
 
 
 def perm_targets_numpy_par(key: np.ndarray, pos: int, n: int, count: int, out: np.ndarray,

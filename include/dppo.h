@@ -289,7 +289,8 @@ int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t coun
  * [2] near-miss records, [3] kept zone words, [4] replayed words, [5] max |offset|, [6] W,
  * [7] Wb, [8] scan us, [9] stitch us, [10] assembly us, [11] slowest chunk us, [12] words
  * generated, [13] failure code, [14] total us, [15] slowest jump-ahead us, [16] words scanned
- * one at a time, [17] disagreeing words applied.  Host only.
+ * one at a time, [17] disagreeing words applied, [18] µs the stitch worked (its waits for chunk
+ * scans excluded).  Host only.
  * Replaces the serial draw behind reference diamond/ppo.py:252-255 (np.random.permutation). */
 int dppo_perm_targets_numpy_par(uint32_t* key, int32_t* pos, int64_t n, int32_t count,
                                 int32_t* out, int32_t threads, const int64_t* opts,

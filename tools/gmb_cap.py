@@ -6,7 +6,8 @@ ppo.py:252-255) and resolves them on its device, while its share of the learn sh
 
 For world = 1, 2, 4, 8:
 * host draw per learn: the serial accept scan (perm.cpp) and the parallel speculative draw
-  (permpar.cpp, DPPO_PERM_PAR_THREADS threads; what dppo_perm_targets_numpy runs), median of 5;
+  (permpar.cpp, DPPO_PERM_PAR_THREADS threads; what dppo_perm_targets_numpy runs), median of 5
+  isolated draws, and of 10 chained ones (back to back, as a host-bound learn draws);
 * on a GPU box: the device time per learn of one rank's share (T x 65,536/world envs, local
   minibatches, the same kernels) plus that rank's global-minibatch member lists from the swap
   targets (dppo_global_minibatch_lists: bucket build over all E x 8.4 M targets, the walk of the
@@ -29,15 +30,19 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "diamond-ppo_amd"))
 
 
-def host_draw_ms(n, epochs=4, reps=5, threads=1):
+def host_draw_ms(n, epochs=4, reps=5, threads=1, chained=False):
+    """Median ms of one draw of the learn's targets.  chained: each draw starts from the previous
+    one's final state, back to back (the look-ahead drafts of a host-bound learn: the draw
+    threads never rest, and the sustained load runs slower than isolated draws on the box)."""
     from diamond import _native as N
     out = np.empty(n * epochs, np.int32)
     ts = []
+    key, pos, _ = N.mt_state(np.random.RandomState(42))
     for r in range(reps + 1):
-        rs = np.random.RandomState(42 + r)
-        key, pos, _ = N.mt_state(rs)
+        if not chained:
+            key, pos, _ = N.mt_state(np.random.RandomState(42 + r))
         t0 = time.perf_counter()
-        N.perm_targets_numpy_par(key, pos, n, epochs, out, threads)
+        pos, _ = N.perm_targets_numpy_par(key, pos, n, epochs, out, threads)
         if r:  # the first draw is a warm-up (buffers, jump polynomials)
             ts.append((time.perf_counter() - t0) * 1e3)
     return float(np.median(ts))
@@ -84,6 +89,7 @@ def main():
     threads = int(os.environ.get("DPPO_PERM_PAR_THREADS", "12"))
     draw_serial = host_draw_ms(T * Ng)
     draw_par = host_draw_ms(T * Ng, threads=threads)
+    draw_chain = host_draw_ms(T * Ng, reps=10, threads=threads, chained=True)
     dev, resolve = {}, None
     if not a.no_gpu:
         import torch
@@ -103,7 +109,8 @@ def main():
     rows = []
     for world in (1, 2, 4, 8):
         row = {"world": world, "host_draw_ms_serial": round(draw_serial, 2),
-               "host_draw_ms_parallel": round(draw_par, 2), "draw_threads": threads,
+               "host_draw_ms_parallel": round(draw_par, 2),
+               "host_draw_ms_parallel_chained": round(draw_chain, 2), "draw_threads": threads,
                "global_samples": T * Ng, "targets_drawn": 4 * T * Ng}
         if dev:
             share = dev[world] - (resolve[1] if world == 1 else 0.0)
@@ -111,7 +118,8 @@ def main():
             row["device_ms_share_local"] = round(share, 3)
             row["device_ms_global_lists"] = round(resolve[world], 3)
             row["device_ms_per_learn_global"] = round(rdev, 3)
-            for tag, draw in (("serial", draw_serial), ("parallel", draw_par)):
+            for tag, draw in (("serial", draw_serial), ("parallel", draw_par),
+                              ("parallel_chained", draw_chain)):
                 bound = max(draw, rdev)
                 row[f"learn_ms_bound_{tag}_draw"] = round(bound, 3)
                 row[f"speedup_cap_{tag}_draw"] = round(dev[1] / bound, 2)
