@@ -79,6 +79,7 @@ struct LoopGroup : LoopSync {
   } while (0)
 
 constexpr int kPermSlots = DPPO_PERM_SLOTS;
+constexpr int kExtSlots = DPPO_PERM_EXT_SLOTS;
 
 struct dppo_handle {
   int device = 0;
@@ -138,6 +139,12 @@ struct dppo_handle {
   int32_t* perms_pinned[kPermSlots] = {};
   hipEvent_t perm_copy_done[kPermSlots] = {};
   bool perm_copy_pending[kPermSlots] = {};
+  // external staging slots (dppo_perm_external): caller-owned host memory, page-locked here,
+  // uploaded from directly -- e.g. a node-shared draw's slots in shared memory
+  int32_t* ext_ptr[kExtSlots] = {};
+  int64_t ext_bytes[kExtSlots] = {};
+  hipEvent_t ext_done[kExtSlots] = {};
+  bool ext_pending[kExtSlots] = {};
   int32_t trace_rows = 0;
   hipStream_t last_stream = nullptr;
   // optional per-kernel-class timing with HIP events on the launch stream
@@ -592,6 +599,21 @@ namespace {
 // pinned slot is copied from directly (pure DMA); any other buffer is first staged in slot 0.
 int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, int ds) {
   const size_t pbytes = (size_t)(h->dims.num_epochs * h->pe) * sizeof(int32_t);
+  for (int k = 0; k < kExtSlots; ++k) {
+    if (!h->ext_ptr[k] || host != h->ext_ptr[k]) continue;
+    if ((int64_t)pbytes > h->ext_bytes[k]) {
+      set_error("external permutation slot %d holds %lld bytes, the learn needs %zu", k,
+                (long long)h->ext_bytes[k], pbytes);
+      return DPPO_EINVAL;
+    }
+    if (h->perms_free_valid[ds])
+      DPPO_HIP_CHECK(hipStreamWaitEvent(h->copy_stream, h->perms_free[ds], 0));
+    DPPO_HIP_CHECK(hipMemcpyAsync(dst, host, pbytes, hipMemcpyHostToDevice, h->copy_stream));
+    DPPO_HIP_CHECK(hipEventRecord(h->ext_done[k], h->copy_stream));
+    DPPO_HIP_CHECK(hipEventRecord(h->perms_ready, h->copy_stream));
+    h->ext_pending[k] = true;
+    return DPPO_OK;
+  }
   int slot = 0;
   for (int k = 1; k < kPermSlots; ++k)
     if (host == h->perms_pinned[k]) slot = k;
@@ -992,6 +1014,10 @@ void dppo_destroy(dppo_handle* h) {
     if (h->perms_pinned[k]) (void)hipHostFree(h->perms_pinned[k]);
     if (h->perm_copy_done[k]) (void)hipEventDestroy(h->perm_copy_done[k]);
   }
+  for (int k = 0; k < kExtSlots; ++k) {
+    if (h->ext_ptr[k]) (void)hipHostUnregister(h->ext_ptr[k]);
+    if (h->ext_done[k]) (void)hipEventDestroy(h->ext_done[k]);
+  }
   for (hipEvent_t e : h->pool) (void)hipEventDestroy(e);
   if (h->err_host) (void)hipHostFree(h->err_host);
   delete h;
@@ -1293,6 +1319,53 @@ int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out) {
     h->perm_copy_pending[slot] = false;
   }
   *out = h->perms_pinned[slot];
+  return DPPO_OK;
+}
+
+int dppo_perm_external(dppo_handle* h, int32_t k, int32_t* ptr, int64_t bytes) {
+  if (!h || k < 0 || k >= kExtSlots || (ptr && bytes <= 0)) {
+    set_error("invalid argument to dppo_perm_external (slot 0..%d)", kExtSlots - 1);
+    return DPPO_EINVAL;
+  }
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  if (h->ext_ptr[k]) {  // the previous registration: its upload must be done before unpinning
+    if (h->ext_pending[k]) DPPO_HIP_CHECK(hipEventSynchronize(h->ext_done[k]));
+    h->ext_pending[k] = false;
+    DPPO_HIP_CHECK(hipHostUnregister(h->ext_ptr[k]));
+    h->ext_ptr[k] = nullptr;
+    h->ext_bytes[k] = 0;
+  }
+  if (!ptr) return DPPO_OK;
+  if (!h->ext_done[k])
+    DPPO_HIP_CHECK(hipEventCreateWithFlags(&h->ext_done[k], hipEventDisableTiming));
+  const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault);
+  if (e != hipSuccess) {
+    set_error("hipHostRegister(%lld bytes) failed: %s", (long long)bytes, hipGetErrorString(e));
+    return DPPO_EHIP;
+  }
+  h->ext_ptr[k] = ptr;
+  h->ext_bytes[k] = bytes;
+  return DPPO_OK;
+}
+
+int dppo_perm_external_done(dppo_handle* h, int32_t k, int32_t* done) {
+  if (!h || !done || k < 0 || k >= kExtSlots) {
+    set_error("invalid argument to dppo_perm_external_done");
+    return DPPO_EINVAL;
+  }
+  *done = 1;
+  if (!h->ext_pending[k]) return DPPO_OK;
+  DPPO_HIP_CHECK(hipSetDevice(h->device));
+  const hipError_t e = hipEventQuery(h->ext_done[k]);
+  if (e == hipErrorNotReady) {
+    *done = 0;
+    return DPPO_OK;
+  }
+  if (e != hipSuccess) {
+    set_error("hipEventQuery: %s", hipGetErrorString(e));
+    return DPPO_EHIP;
+  }
+  h->ext_pending[k] = false;
   return DPPO_OK;
 }
 

@@ -23,13 +23,14 @@ MAX_TENSORS = 16
 GAE_EXACT, GAE_AFFINE = 0, 1  # dppo_set_gae_mode
 TRACE_FIELDS = 5
 PERM_SLOTS = 3  # pinned permutation staging slots per handle (include/dppo.h DPPO_PERM_SLOTS)
+PERM_EXT_SLOTS = 8  # external (caller-owned) staging slots per handle (DPPO_PERM_EXT_SLOTS)
 
 EXPORTED = [
     "dppo_version", "dppo_last_error", "dppo_param_layout", "dppo_create", "dppo_destroy",
     "dppo_gae_f32", "dppo_gae_stream_probe", "dppo_set_gae_mode", "dppo_adv_stats", "dppo_adv_sums", "dppo_adv_stats_from_sums",
     "dppo_adv_normalize_f32", "dppo_old_policy_f32",
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
-    "dppo_perm_buffer", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
+    "dppo_perm_buffer", "dppo_perm_external", "dppo_perm_external_done", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
     "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_global_minibatch_lists", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
@@ -131,6 +132,8 @@ def load():
         "dppo_clip_adam_f32": (ctypes.c_int, [vp, vp, vp, vp, i64, f32, f64, f32, f32, f32, i64,
                                               vp, vp]),
         "dppo_perm_buffer": (ctypes.c_int, [vp, i32, P(vp)]),
+        "dppo_perm_external": (ctypes.c_int, [vp, i32, vp, i64]),
+        "dppo_perm_external_done": (ctypes.c_int, [vp, i32, P(i32)]),
         "dppo_get_trace": (ctypes.c_int, [vp, vp, i32]),
         "dppo_perm_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
         "dppo_perm_targets_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
@@ -338,6 +341,18 @@ class Handle:
         p = ctypes.c_void_p()
         check(self.lib.dppo_perm_buffer(self.h, int(slot), ctypes.byref(p)), "dppo_perm_buffer")
         return p.value
+
+    def perm_external(self, k: int, ptr: int | None, nbytes: int = 0):
+        """Register caller-owned host memory as external staging slot ``k`` (page-locked by the
+        handle, uploaded from directly); ``ptr=None`` unregisters it."""
+        check(self.lib.dppo_perm_external(self.h, int(k), ptr, int(nbytes)), "dppo_perm_external")
+
+    def perm_external_done(self, k: int) -> bool:
+        """True once the last upload from external slot ``k`` has completed (non-blocking)."""
+        d = ctypes.c_int32()
+        check(self.lib.dppo_perm_external_done(self.h, int(k), ctypes.byref(d)),
+              "dppo_perm_external_done")
+        return bool(d.value)
 
     def trace(self, rows: int) -> np.ndarray:
         out = np.zeros((rows, TRACE_FIELDS), np.float32)

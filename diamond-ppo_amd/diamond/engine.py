@@ -407,6 +407,16 @@ class NativeLearner:
         self._slot = 0
         self._worker = None
         self._closed = False
+        # global minibatches: the node's ranks share one draw per learn (drawshare.py;
+        # DPPO_PERM_SHARE=0 keeps one draw per rank)
+        self.share = None
+        self._cur_share = None
+        d = torch.distributed
+        if (self.global_mb and self.device_shuffle and self.lookahead and not _SOLO[0]
+                and os.environ.get("DPPO_PERM_SHARE", "1") != "0"
+                and d.is_available() and d.is_initialized()):
+            from . import drawshare
+            self.share = drawshare.setup(d, self)
 
     def _init_comm(self):
         """The rank exchange of the data-parallel learn.  DPPO_COMM: "auto" (default) = an RCCL
@@ -586,6 +596,8 @@ class NativeLearner:
         buf = d["buf"] = self.handle.perm_buffer(slot)
         self.host_seconds["slot_wait"] += time.perf_counter() - t0
 
+        share = self.share
+
         def work():
             if prev is not None:
                 if not prev["ok"]:
@@ -593,7 +605,23 @@ class NativeLearner:
                 d["key_in"], d["pos_in"] = prev["key_out"].copy(), prev["pos_out"]
             t1 = time.perf_counter()
             k = d["key_in"].copy()
-            if device_shuffle:
+            if device_shuffle and share is not None:
+                # one draw per node: the leader draws into a shared slot, the others take it
+                # when it is the draw of their own state (else draw it themselves)
+                if share.leader:
+                    sl, gen, d["pos_out"] = share.lead(
+                        k, d["pos_in"], lambda kk, pp, view: draw(kk, pp, perm_n, epochs, view))
+                    d["buf"], d["share"] = share.ptr(sl), (sl, gen)
+                else:
+                    r = share.follow(k, d["pos_in"])
+                    if r is not None:
+                        sl, gen, key_out, d["pos_out"] = r
+                        k[:] = key_out
+                        d["buf"], d["share"] = share.ptr(sl), (sl, gen)
+                    else:
+                        share.stats["own"] += 1
+                        d["pos_out"] = draw(k, d["pos_in"], perm_n, epochs, buf)
+            elif device_shuffle:
                 d["pos_out"] = draw(k, d["pos_in"], perm_n, epochs, buf)
             else:
                 # returns after the draws: the last epochs' swaps finish on the host pool while
@@ -636,6 +664,9 @@ class NativeLearner:
             if self._worker is not None:
                 self._worker.stop()
                 self._worker = None
+            if self.share is not None:  # unregisters its slots from the handle first
+                self.share.close()
+                self.share = None
             self.handle.close()
 
     def __del__(self):
@@ -657,6 +688,7 @@ class NativeLearner:
             if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos
                     and np.array_equal(d["key_in"], key)):
                 self._slot = d["slot"]
+                self._cur_share = d.get("share")
                 N.set_mt_state(st, d["key_out"], d["pos_out"])
                 self.host_seconds["lookahead_hits"] += 1
                 return d["buf"], d["key_out"], d["pos_out"]
@@ -683,6 +715,9 @@ class NativeLearner:
         if self.fused:
             t0 = time.perf_counter()
             stream = torch.cuda.current_stream(self.device).cuda_stream
+            if self.share is not None:
+                self.share.pump()  # release the shared slots whose uploads are done
+            self._cur_share = None
             pinned, key, pos = self._targets()
             t1 = time.perf_counter()
             # the next learns' draws overlap this learn's enqueue and device time
@@ -699,6 +734,8 @@ class NativeLearner:
                        self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
                        ctypes.byref(outputs) if outputs is not None else None, stream),
                     "dppo_learn_f32")
+            if self._cur_share is not None:  # its upload from the shared slot is now enqueued
+                self.share.used(*self._cur_share)
             t3 = time.perf_counter()
             hs = self.host_seconds
             hs["perms"] += t1 - t0

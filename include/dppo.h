@@ -241,6 +241,17 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
 #define DPPO_PERM_SLOTS 3
 int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out);
 
+/* External staging slots (round 5): caller-owned host memory of `bytes` (e.g. a slot of a
+ * node-shared draw in POSIX shared memory) page-locked by the handle (hipHostRegister) as slot
+ * k (0..DPPO_PERM_EXT_SLOTS-1), so that dppo_learn_f32 / dppo_learn_targets_f32 given that
+ * pointer upload from it directly; ptr = NULL unregisters (after the slot's last upload).
+ * dppo_perm_external_done: *done = 1 once the last upload from slot k has completed (a
+ * non-blocking event query).  Replaces nothing in the reference: the shared-draw plumbing of
+ * ppo.py:252-255 across a node's ranks. */
+#define DPPO_PERM_EXT_SLOTS 8
+int dppo_perm_external(dppo_handle* h, int32_t k, int32_t* ptr, int64_t bytes);
+int dppo_perm_external_done(dppo_handle* h, int32_t k, int32_t* done);
+
 /* Per-kernel timing with HIP events (off by default): while enabled, every kernel the handle
  * launches carries a start/stop event pair stamped with the kernel's own execution interval
  * (hipExtLaunchKernel), RCCL calls a pair of stream markers.  Classes, in order: old-policy eval,

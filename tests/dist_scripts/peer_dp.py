@@ -130,6 +130,46 @@ def run_agent(rank, world, out):
     L.close()
 
 
+def run_share(rank, world, out):
+    """Global minibatches with the swap targets drawn on the host (DPPO_PERM_DEVICE=1): the same
+    four learns from the same parameters and NumPy state, first with one draw per rank
+    (DPPO_PERM_SHARE=0), then with the node-shared draw (drawshare.py: rank 0 draws into shared
+    memory, rank 1 uploads from it)."""
+    import torch
+    import diamond
+    import bench
+    from gpu_helpers import SpecEnvs
+    T, Nl, D, A, n_learn = 32, 64, 4, 2, 4
+    res = {}
+    init = None
+    for tag, share in (("own", "0"), ("shared", "1")):
+        os.environ["DPPO_PERM_SHARE"] = share
+        cfg = diamond.PPOConfig(rollout_steps=T, num_envs=Nl, verbose=False,
+                                global_minibatches=True)
+        agent = diamond.PPO(None, cfg, envs=SpecEnvs(D, A, False))
+        L = agent._learner
+        assert L.global_mb and L.device_shuffle and L.lookahead
+        assert (L.share is not None) == (share == "1"), L.share
+        if init is None:
+            init = L.flat.flat.detach().clone()
+        else:
+            L.flat.flat.copy_(init)
+        ro, _ = bench.synth_rollout(T, Nl, D, A, False, 0.02, 0.005, rank, agent.device)
+        np.random.seed(7)
+        for _ in range(n_learn):
+            agent.learn_device(ro)
+        torch.cuda.synchronize()
+        res[f"final_{tag}"] = L.flat.flat.cpu().numpy()
+        res[f"trace_{tag}"] = agent.learn_trace()
+        res[f"rng_{tag}"] = np.random.get_state()[1].copy()
+        if L.share is not None:
+            st = L.share.stats
+            res["stats"] = np.array([st["shared"], st["own"], st["mismatch"], st["timeout"],
+                                     int(L.share.leader)])
+        L.close()
+    np.savez(out, **res)
+
+
 def run_dead(rank, world, out):
     """Rank 1 stops exchanging after the self-test (it sleeps past DPPO_PEER_TIMEOUT_S, as a
     hung or crashed peer would): rank 0's learn() must end with the peer-timeout error
@@ -194,7 +234,7 @@ def run(rank, world, port, kind, out, env=None):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        {"handle": run_handle, "agent": run_agent, "dead": run_dead,
+        {"handle": run_handle, "agent": run_agent, "dead": run_dead, "share": run_share,
          "selftest_fail": run_selftest_fail}[kind](rank, world, out)
         dist.barrier()
     finally:

@@ -1,0 +1,112 @@
+"""The node-shared draw (diamond/drawshare.py) across real processes, on the CPU: a leader draws
+the learner's chain of look-ahead drafts (NumPy-exact Fisher-Yates swap targets, the
+``dppo_perm_targets_numpy`` path of a global-minibatch learn) into shared-memory slots; a
+follower with the same NumPy state takes every draft and gets bit for bit its own draw (targets,
+MT19937 key and pos); a follower whose state differs never takes one, draws itself, and never
+holds the leader back.  The handle is a stand-in whose uploads complete at once."""
+import multiprocessing as mp
+import os
+import uuid
+
+import numpy as np
+import pytest
+
+from conftest import PKG  # noqa: F401  (puts diamond-ppo_amd on sys.path)
+
+N_SAMPLES, EPOCHS, DRAFTS = 4096, 3, 9
+
+
+class _Handle:
+    def perm_external(self, k, ptr, nbytes=0):
+        pass
+
+    def perm_external_done(self, k):
+        return True
+
+
+def _run(name, create, me, nloc, seed, q, bar):
+    from diamond import _native as N
+    from diamond import drawshare as S
+    try:
+        share = S.NodeDrawShare(name, create, me, nloc, EPOCHS * N_SAMPLES * 4, _Handle())
+        bar.wait(60)  # every rank attached (engine: setup()'s agreement collective)
+        key, pos, _ = N.mt_state(np.random.RandomState(seed))
+        taken, ok = 0, True
+        for _ in range(DRAFTS):
+            mine_key = key.copy()
+            mine = np.empty(EPOCHS * N_SAMPLES, np.int32)
+            mine_pos = N.perm_targets_numpy(mine_key, pos, N_SAMPLES, EPOCHS, mine)
+            if share.leader:
+                sl, gen, pos = share.lead(
+                    key, pos, lambda kk, pp, view: N.perm_targets_numpy(kk, pp, N_SAMPLES,
+                                                                         EPOCHS, view))
+                got = share.views[sl][:EPOCHS * N_SAMPLES]
+                ok &= bool(np.array_equal(got, mine)) and pos == mine_pos
+                share.used(sl, gen)
+            else:
+                r = share.follow(key, pos)
+                if r is not None:
+                    sl, gen, key_out, pos_out = r
+                    ok &= bool(np.array_equal(share.views[sl][:EPOCHS * N_SAMPLES], mine))
+                    ok &= bool(np.array_equal(key_out, mine_key)) and pos_out == mine_pos
+                    share.used(sl, gen)
+                    taken += 1
+                key, pos = mine_key, mine_pos
+            if share.leader:
+                ok &= bool(np.array_equal(key, mine_key))
+            share.pump()
+        stats = dict(share.stats)
+        bar.wait(60)  # nobody closes (the leader unlinks) while another rank still reads
+        share.close()
+        q.put((me, ok, taken, stats))
+    except Exception as e:  # reported to the parent
+        q.put((me, False, -1, repr(e)))
+
+
+def _spawn(seeds):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    bar = ctx.Barrier(len(seeds))
+    name = f"dppo_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    nloc = len(seeds)
+    # the leader creates the segment before the followers attach
+    lead = ctx.Process(target=_run, args=(name, True, 0, nloc, seeds[0], q, bar))
+    lead.start()
+    import time
+    for _ in range(200):
+        if os.path.exists(f"/dev/shm/{name}"):
+            break
+        time.sleep(0.05)
+    rest = [ctx.Process(target=_run, args=(name, False, r, nloc, seeds[r], q, bar))
+            for r in range(1, nloc)]
+    for p in rest:
+        p.start()
+    out = {}
+    for _ in range(nloc):
+        me, ok, taken, stats = q.get(timeout=120)
+        out[me] = (ok, taken, stats)
+    for p in [lead] + rest:
+        p.join(30)
+    assert all(p.exitcode == 0 for p in [lead] + rest)
+    return out
+
+
+@pytest.mark.timeout(180)
+def test_followers_take_the_leaders_draws_bit_exact():
+    out = _spawn([11, 11, 11])
+    for r, (ok, taken, stats) in out.items():
+        assert ok, (r, stats)
+        if r:
+            assert taken == DRAFTS and stats["shared"] == DRAFTS, stats
+
+
+@pytest.mark.timeout(180)
+def test_a_follower_with_another_state_draws_itself_and_never_blocks_the_leader():
+    os.environ["DPPO_PERM_SHARE_TIMEOUT_S"] = "20"
+    try:
+        out = _spawn([11, 11, 12])
+    finally:
+        del os.environ["DPPO_PERM_SHARE_TIMEOUT_S"]
+    assert out[0][0] and out[1][0] and out[2][0]
+    assert out[1][1] == DRAFTS            # the matching follower took every draft
+    assert out[2][1] == 0 and out[2][2]["mismatch"] + out[2][2]["timeout"] == DRAFTS

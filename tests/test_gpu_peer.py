@@ -98,6 +98,23 @@ def test_failing_peer_selftest_is_refused_on_every_rank(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_node_shared_draw_matches_one_draw_per_rank(tmp_path):
+    """Global minibatches with host-drawn swap targets: the node-shared draw (rank 0 draws into
+    shared memory, rank 1 uploads from it, drawshare.py) gives bit for bit the parameters, traces
+    and NumPy state of one draw per rank, and rank 1 did take rank 0's drafts."""
+    r0, r1 = _spawn("share", tmp_path, env={"DPPO_PERM_DEVICE": "1",
+                                            "DPPO_PERM_SHARE_TIMEOUT_S": "30"})
+    for r in (r0, r1):
+        assert np.array_equal(r["final_own"], r["final_shared"])
+        assert np.array_equal(r["trace_own"], r["trace_shared"])
+        assert np.array_equal(r["rng_own"], r["rng_shared"])
+    assert np.array_equal(r0["final_shared"], r1["final_shared"])
+    shared, own, mismatch, timeout, leader = (int(x) for x in r1["stats"])
+    assert leader == 0 and shared >= 3 and own == 0 and timeout == 0, r1["stats"]
+    assert int(r0["stats"][4]) == 1 and int(r0["stats"][0]) >= 3, r0["stats"]
+
+
+@pytest.mark.timeout(300)
 def test_peer_exchange_drop_in_agent(tmp_path):
     r0, r1 = _spawn("agent", tmp_path)
     assert np.array_equal(r0["init"], r1["init"])
