@@ -331,6 +331,8 @@ class _DraftWorker:
                 return
             try:
                 fn()
+            except Exception as e:  # the draft stays not-ok: its learn redraws on its own thread
+                warnings.warn(f"permutation draft failed ({e!r}); the learn draws it itself")
             finally:
                 done.set()
             # the finished job's closure must not outlive it: it holds the draft's buffers

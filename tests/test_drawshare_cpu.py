@@ -110,3 +110,25 @@ def test_a_follower_with_another_state_draws_itself_and_never_blocks_the_leader(
     assert out[0][0] and out[1][0] and out[2][0]
     assert out[1][1] == DRAFTS            # the matching follower took every draft
     assert out[2][1] == 0 and out[2][2]["mismatch"] + out[2][2]["timeout"] == DRAFTS
+
+
+def test_a_failing_draft_does_not_stop_the_draft_worker():
+    """A draft whose job raises (e.g. the shared draw's bounded wait) leaves the worker running:
+    later drafts still run and signal completion (before, the worker thread died with the
+    exception and the next learn waited forever)."""
+    import threading
+    import warnings
+    from diamond.engine import _DraftWorker
+    w = _DraftWorker()
+    ran = []
+    d1, d2 = threading.Event(), threading.Event()
+
+    def bad():
+        raise RuntimeError("slot not released")
+
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        w.submit(bad, d1)
+        w.submit(lambda: ran.append(1), d2)
+        assert d1.wait(10) and d2.wait(10) and ran == [1]
+    w.stop()

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--chunks-per-thread", type=int, default=0,
                     help="chunks = this x threads (0: the library default, 2 per thread)")
     ap.add_argument("--chain", type=int, default=0)
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="idle time between chained draws (a device-bound learn's gaps)")
     ap.add_argument("--pinned", action="store_true",
                     help="draw into page-locked host memory (torch pin_memory, i.e. hipHostMalloc: "
                          "what the learner's upload slots are) instead of a NumPy array")
@@ -100,6 +102,8 @@ def main():
             kk, pp = key0.copy(), pos0
             ts = []
             for _ in range(a.chain):
+                if a.gap_ms > 0:
+                    time.sleep(a.gap_ms * 1e-3)
                 t0 = time.perf_counter()
                 pp, _ = N.perm_targets_numpy_par(kk, pp, n, E, got, thr, chunks=ch)
                 ts.append((time.perf_counter() - t0) * 1e3)
@@ -118,6 +122,7 @@ def main():
                "fallbacks": sum(1 for r in rows if r["path"] != 1),
                "all_bit_exact": all(r["bit_exact"] for r in rows)}
     if chained:
+        summary["gap_ms"] = a.gap_ms
         summary["chained_ms_median"] = {t: med(v[1:]) for t, v in chained.items()}
         summary["chained_ms_min"] = {t: round(min(v[1:]), 3) for t, v in chained.items()}
     print(json.dumps(summary), flush=True)
