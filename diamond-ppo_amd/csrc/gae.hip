@@ -300,7 +300,29 @@ __device__ __forceinline__ int pipe_tile(int lb, int ntiles) {
   return (grp + 1) * G <= ntiles ? grp * G + K * (r & 7) + (r >> 3) : lb;
 }
 
-template <int E>
+// The streaming variants of the owners' global accesses and the tile map (NT bits, A/B via
+// DPPO_GAE_NT; tools/probe/stream_probe2.hip measured each on the launch's bare data movement):
+//   1 non-temporal operand loads, 2 non-temporal advantage / return stores,
+//   4 XCD-contiguous tiles: the blocks one XCD runs (round-robin dispatch) take one contiguous
+//     eighth of the env axis (groups of K = 128 / E tiles sharing a flag line stay on one XCD)
+template <int NT, typename T>
+__device__ __forceinline__ T gld(const T* p) {
+  if (NT & 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <int NT, typename T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  if (NT & 2) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <int E, int NT>
+__device__ __forceinline__ int pipe_tile_nt(int lb, int ntiles) {
+  constexpr int K = 128 / E;
+  if ((NT & 4) && ntiles % (8 * K) == 0) return (lb % 8) * (ntiles / 8) + lb / 8;
+  return pipe_tile<E>(lb, ntiles);
+}
+
+template <int E, int NT = 0>
 __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
     const float* __restrict__ rew, const uint8_t* __restrict__ term,
     const uint8_t* __restrict__ trunc, const float* __restrict__ val,
@@ -337,7 +359,7 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
       while ((long long)__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(2);
     }
     for (int lb = blockIdx.x; lb < ntiles; lb += gridDim.x) {
-      const int n0 = pipe_tile<E>(lb, ntiles) * E;
+      const int n0 = pipe_tile_nt<E, NT>(lb, ntiles) * E;
       for (int s = 0; s < nsup; ++s) {
         ++gen;
         const int hi = T - s * kPSuper;
@@ -353,11 +375,11 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
           const int row = p * RP + lane / V4;
           if (row < nr) {
             const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
-            xr[p] = *(const f32x4*)(rew + go);
-            xv[p] = *(const f32x4*)(val + go);
-            xn[p] = *(const f32x4*)(nval + go);
-            xt[p] = *(const uint32_t*)(term + go);
-            xu[p] = *(const uint32_t*)(trunc + go);
+            xr[p] = gld<NT>((const f32x4*)(rew + go));
+            xv[p] = gld<NT>((const f32x4*)(val + go));
+            xn[p] = gld<NT>((const f32x4*)(nval + go));
+            xt[p] = gld<NT>((const uint32_t*)(term + go));
+            xu[p] = gld<NT>((const uint32_t*)(trunc + go));
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -410,8 +432,8 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
               store_wt(adv + go, av);
               store_wt(ret + go, xv[p] + av);  // returns = values + advantages (ppo.py:241)
             } else {
-              *(f32x4*)(adv + go) = av;
-              *(f32x4*)(ret + go) = xv[p] + av;
+              gst<NT>((f32x4*)(adv + go), av);
+              gst<NT>((f32x4*)(ret + go), xv[p] + av);
             }
             stats4(av, sft, s32, q32);
             cnt += 4;
@@ -986,6 +1008,30 @@ extern "C" __attribute__((visibility("default"))) int dppo_debug_gae_trace(long 
 }
 #endif
 
+// gae_pipe_kernel<E, NT> for the DPPO_GAE_NT variant
+template <int E, int NT>
+int launch_pipe_nt(int grid, hipStream_t s, const float* r, const uint8_t* te, const uint8_t* tr,
+                   const float* v, const float* nv, float* adv, float* ret, double* partials,
+                   int T, int N, float gamma, float c, int wt, int stagger, int psleep) {
+  const auto kern = gae_pipe_kernel<E, NT>;
+  DPPO_LAUNCH(kern, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv, adv, ret, partials, T,
+              N, gamma, c, wt, stagger, psleep);
+  DPPO_LAUNCH_CHECK();
+  return DPPO_OK;
+}
+template <int E>
+int launch_pipe(int nt, int grid, hipStream_t s, const float* r, const uint8_t* te,
+                const uint8_t* tr, const float* v, const float* nv, float* adv, float* ret,
+                double* partials, int T, int N, float gamma, float c, int wt, int stagger,
+                int psleep) {
+  switch (nt) {
+    case 3: return launch_pipe_nt<E, 3>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+    case 4: return launch_pipe_nt<E, 4>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+    case 7: return launch_pipe_nt<E, 7>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+    default: return launch_pipe_nt<E, 0>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+  }
+}
+
 int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float* v,
                const float* nv, float* adv, float* ret, double* partials, int T, int N,
                float gamma, float gae_lambda, hipStream_t s, int* n_partials, int mode) {
@@ -1029,6 +1075,13 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     // DPPO_GAE_PSLEEP=0/1/2 overrides (A/B).
     static const int psleep =
         std::getenv("DPPO_GAE_PSLEEP") ? std::atoi(std::getenv("DPPO_GAE_PSLEEP")) : 1;
+    // DPPO_GAE_NT: the owners' streaming variant (gae_pipe_kernel NT bits; 0, 3, 4 or 7; A/B).
+    // On cold rotating buffers (tools/gae_bench.py) non-temporal operand loads and advantage /
+    // return stores (3) measured 7.25-7.59 against 7.73-7.84 us per launch at N = 8192; inside a
+    // learn, where the eval kernel has just written values / next_values and the pack kernel reads
+    // the advantages next, they cost: GAE 8.2-8.3 against 7.0-7.25 us, pack 23.7-24.8 against
+    // 19.4 us at C3 (tools/gpu/r05_gae_nt_learn.sh).  Plain accesses stay the default.
+    static const int nt = std::getenv("DPPO_GAE_NT") ? std::atoi(std::getenv("DPPO_GAE_NT")) : 0;
     const int tiles = e64 ? N / 64 : (e32 ? N / 32 : G);
     int grid = tiles < per_cu * cus ? tiles : per_cu * cus;
     if (!e32 && grid >= 16) grid -= grid % 16;
@@ -1038,8 +1091,7 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
         DPPO_LAUNCH(gae_aff_kernel<64>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
                     nv, adv, ret, partials, T, N, gamma, c, stagger);
       else
-        DPPO_LAUNCH(gae_pipe_kernel<64>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                    adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+        { const int rc_ = launch_pipe<64>(nt, grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep); if (rc_ != DPPO_OK) return rc_; }
     } else if (mode == DPPO_GAE_AFFINE) {
       if (e32)
         DPPO_LAUNCH(gae_aff_kernel<32>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
@@ -1048,11 +1100,9 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
         DPPO_LAUNCH(gae_aff_kernel<16>, dim3(grid), dim3(kPChunks * kWave), 0, s, r, te, tr, v,
                     nv, adv, ret, partials, T, N, gamma, c, stagger);
     } else if (e32)
-      DPPO_LAUNCH(gae_pipe_kernel<32>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+      { const int rc_ = launch_pipe<32>(nt, grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep); if (rc_ != DPPO_OK) return rc_; }
     else
-      DPPO_LAUNCH(gae_pipe_kernel<16>, dim3(grid), dim3(kPThreads), 0, s, r, te, tr, v, nv,
-                  adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+      { const int rc_ = launch_pipe<16>(nt, grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep); if (rc_ != DPPO_OK) return rc_; }
   } else if (vec)
     DPPO_LAUNCH(gae_kernel<true>, dim3(G), dim3(kThreads), 0, s, r, te, tr, v, nv, adv, ret,
                        partials, T, N, gamma, c);
