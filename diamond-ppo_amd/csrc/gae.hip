@@ -1115,22 +1115,47 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
 
 // ---- The streaming ceiling of the GAE launch (measurement only, dppo_gae_stream_probe): the
 // same 22 B per element over the same [T][N] buffers -- read rewards, values, next_values (16 B
-// per lane) and the two flag bytes, write advantages and returns -- with no recurrence, one
-// persistent grid like gae_pipe_kernel's.  What one launch of these bytes reaches on this part
-// (bench.py roofline_gae: ceiling_us, frac_of_ceiling).
+// per lane) and the two flag bytes, write advantages and returns -- with no recurrence, in the
+// fastest pattern measured for one cold launch of these bytes (tools/probe/stream_probe2.hip, mode
+// 7: non-temporal loads and stores, two elements per thread, each XCD's blocks on one contiguous
+// eighth of the buffers; 6.4 against 7.6 us for plain accesses at N = 8192).  What one launch of
+// these bytes reaches on this part (bench.py roofline_gae: ceiling_us, frac_of_ceiling).
 __global__ __launch_bounds__(256) void gae_stream_probe_kernel(
     const float* __restrict__ r, const uint8_t* __restrict__ te, const uint8_t* __restrict__ tr,
     const float* __restrict__ v, const float* __restrict__ nv, float* __restrict__ adv,
     float* __restrict__ ret, int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const f32x4 a = ((const f32x4*)r)[i];
-    const f32x4 b = ((const f32x4*)v)[i];
-    f32x4 o = ((const f32x4*)nv)[i];
-    const uint32_t t = ((const uint32_t*)te)[i];
-    const uint32_t u = ((const uint32_t*)tr)[i];
-    o[0] += (float)((t ^ u) & 0xffu);
-    ((f32x4*)adv)[i] = a + b;
-    ((f32x4*)ret)[i] = o;
+  const int64_t g = gridDim.x;
+  const int64_t b = (g % 8 == 0) ? ((int64_t)blockIdx.x % 8) * (g / 8) + blockIdx.x / 8
+                                 : (int64_t)blockIdx.x;
+  const int64_t per = n4 / 2;
+  for (int64_t i = b * 256 + threadIdx.x; i < per; i += g * 256) {
+    f32x4 a[2], bb[2], c[2];
+    uint32_t t[2], u[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t k = i + e * per;
+      a[e] = __builtin_nontemporal_load((const f32x4*)r + k);
+      bb[e] = __builtin_nontemporal_load((const f32x4*)v + k);
+      c[e] = __builtin_nontemporal_load((const f32x4*)nv + k);
+      t[e] = __builtin_nontemporal_load((const uint32_t*)te + k);
+      u[e] = __builtin_nontemporal_load((const uint32_t*)tr + k);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int64_t k = i + e * per;
+      f32x4 o = c[e];
+      o[0] += (float)((t[e] ^ u[e]) & 0xffu);
+      __builtin_nontemporal_store(a[e] + bb[e], (f32x4*)adv + k);
+      __builtin_nontemporal_store(o, (f32x4*)ret + k);
+    }
+  }
+  // (n4 odd: the last element)
+  if ((n4 & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t k = n4 - 1;
+    f32x4 o = ((const f32x4*)nv)[k];
+    o[0] += (float)((((const uint32_t*)te)[k] ^ ((const uint32_t*)tr)[k]) & 0xffu);
+    ((f32x4*)adv)[k] = ((const f32x4*)r)[k] + ((const f32x4*)v)[k];
+    ((f32x4*)ret)[k] = o;
   }
 }
 
@@ -1146,8 +1171,10 @@ int launch_gae_stream_probe(const float* r, const uint8_t* te, const uint8_t* tr
       cus = 256;
   }
   const int64_t n4 = n / 4;
-  int64_t grid = (n4 + 255) / 256;
-  if (grid > 4 * cus) grid = 4 * cus;  // 1,024 on 256 CUs: the probe's best (profiles/r02_*)
+  int64_t grid = (n4 / 2 + 255) / 256;
+  if (grid > 2 * cus) grid = 2 * cus;  // 512 on 256 CUs (stream_probe2: 256 and 512 level)
+  if (grid >= 8) grid -= grid % 8;
+  if (grid < 1) grid = 1;
   DPPO_LAUNCH(gae_stream_probe_kernel, dim3((unsigned)grid), dim3(256), 0, s, r, te, tr, v, nv,
               adv, ret, n4);
   DPPO_LAUNCH_CHECK();
