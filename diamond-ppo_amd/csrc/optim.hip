@@ -51,7 +51,18 @@ __device__ __forceinline__ float slab_sum(const float* __restrict__ slabs, int G
     for (; g + (kSlabBatch - 1) * kRedWaves < G; g += kSlabBatch * kRedWaves) {
       float x[kSlabBatch];
 #pragma unroll
-      for (int k = 0; k < kSlabBatch; ++k) x[k] = src[(int64_t)(g + kRedWaves * k) * stride];
+      for (int k = 0; k < kSlabBatch; ++k) {
+        // Non-temporal slab reads (each slab float is read once).  They cost this kernel
+        // ~0.1-0.25 us, and the next minibatch kernel launch gains: C2 53.3 -> 51.4-51.5 us (0.593
+        // -> 0.614 of peak), C4 59.7-59.9 -> 58.8-58.9 us, C3 / C5 unchanged (tools/gpu/
+        // r05_ra_nt2.sh, 2 A/B pairs) -- the slab lines no longer displace what that launch
+        // re-reads from L2.  -DDPPO_RA_PLAIN restores plain reads (A/B).
+#ifdef DPPO_RA_PLAIN
+        x[k] = src[(int64_t)(g + kRedWaves * k) * stride];
+#else
+        x[k] = __builtin_nontemporal_load(src + (int64_t)(g + kRedWaves * k) * stride);
+#endif
+      }
 #pragma unroll
       for (int k = 0; k < kSlabBatch; ++k) s += x[k];
     }
