@@ -525,7 +525,13 @@ __device__ __forceinline__ void slab_st4(float* p, f32x4 v) {
   // s_nop: a VALU write to the data VGPRs of a store wider than 8 bytes needs a wait state
   // after it, which the compiler cannot insert behind an asm statement (seen: back-to-back slab
   // stores whose next operands overwrote this one's data before it was read)
+#if defined(DPPO_SLAB_NT_SC1)  // (A/B) the non-temporal cache policy on top
+  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#elif defined(DPPO_SLAB_NT)  // (A/B) non-temporal instead of write-through
+  asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#else
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#endif
 }
 
 __device__ __forceinline__ f32x4 z4() { return (f32x4){0.f, 0.f, 0.f, 0.f}; }
