@@ -622,12 +622,17 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     return f;
   };
   // a group's layer-1 inputs (N layout) ...
+#ifdef DPPO_GATHER_NT  // (A/B) the record gathers with the non-temporal cache policy
+#define GLD(p) __builtin_nontemporal_load(p)
+#else
+#define GLD(p) (*(p))
+#endif
   auto gather_xn = [&](const Fetch& f, GRec<NIB>& g) {
     const float* rn = a.rec + (int64_t)f.sn * R;
 #pragma unroll
     for (int t = 0; t < 4 * NIB; ++t) {
       const int c = 4 * t + q;
-      g.xn[t] = rn[c < D ? c : D - 1];
+      g.xn[t] = GLD(rn + (c < D ? c : D - 1));
     }
   };
   // ... and the rest of its records
@@ -638,11 +643,11 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int c = 16 * ib + r;
-        g.xt[ib][v] = kLateXt ? 0.f : a.rec[(int64_t)f.st[v] * R + (c < D ? c : D - 1)];
+        g.xt[ib][v] = kLateXt ? 0.f : GLD(a.rec + (int64_t)f.st[v] * R + (c < D ? c : D - 1));
       }
-    g.sc = *(const f32x4*)(rn + a.D8);
-    g.ca[0] = CONT && !kLateCa ? *(const f32x4*)(rn + a.D8 + 4) : z4();
-    g.ca[1] = (CONT && !kLateCa && AMAX > 4) ? *(const f32x4*)(rn + a.D8 + 8) : z4();
+    g.sc = GLD((const f32x4*)(rn + a.D8));
+    g.ca[0] = CONT && !kLateCa ? GLD((const f32x4*)(rn + a.D8 + 4)) : z4();
+    g.ca[1] = (CONT && !kLateCa && AMAX > 4) ? GLD((const f32x4*)(rn + a.D8 + 8)) : z4();
     g.sn = f.sn;
   };
   auto gather = [&](const Fetch& f) {
@@ -874,8 +879,8 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
     float out[AMAX];
     if (kLateCa) {
       const float* rn = a.rec + (int64_t)g_cur.sn * R + a.D8;
-      g_cur.ca[0] = *(const f32x4*)(rn + 4);
-      g_cur.ca[1] = *(const f32x4*)(rn + 8);
+      g_cur.ca[0] = GLD((const f32x4*)(rn + 4));
+      g_cur.ca[1] = GLD((const f32x4*)(rn + 8));
     }
     // the head rows this lane dots (actor heads and the value head), read before the critic
     // layer's MFMAs: read at their use, every row cost one exposed LDS round trip (the scheduler
@@ -1223,7 +1228,7 @@ __global__ __launch_bounds__(kThreadsW, 1) void mbw_kernel(WArgs a) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int c = 16 * ib + r;
-          g_cur.xt[ib][v] = a.rec[(int64_t)st[v] * R + (c < D ? c : D - 1)];
+          g_cur.xt[ib][v] = GLD(a.rec + (int64_t)st[v] * R + (c < D ? c : D - 1));
         }
     }
     f32x4 dh2[4] = {z4(), z4(), z4(), z4()};
