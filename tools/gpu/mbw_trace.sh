@@ -4,6 +4,6 @@
 set -o pipefail
 mkdir -p gpurun_out/trace
 for C in ${1:-cartpole4096 lunar8192 cheetah4096}; do
-  PHASE_CONFIG=$C DPPO_LIB=diamond-ppo_amd/build/libdppo_trace.so WARM_LAUNCHES=20000 timeout -k 10 200 python tools/mbw_trace.py > gpurun_out/trace/$C.txt 2>&1 || exit 1
+  PHASE_CONFIG=$C DPPO_LIB=${TRACE_LIB:-diamond-ppo_amd/ab/libdppo_trace.so} WARM_LAUNCHES=20000 timeout -k 10 200 python tools/mbw_trace.py > gpurun_out/trace/$C.txt 2>&1 || exit 1
   echo "== $C"; cat gpurun_out/trace/$C.txt | grep -v amdgpu.ids
 done
