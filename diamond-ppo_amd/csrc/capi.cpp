@@ -128,7 +128,8 @@ struct dppo_handle {
   int32_t* perms_dev2[2] = {nullptr, nullptr};
   int32_t* targets_dev2[2] = {nullptr, nullptr};
   int32_t* perms_dev = nullptr;     // the buffer of the learn being enqueued
-  int32_t* perm_scratch = nullptr;  // [3][E][B] Fisher-Yates resolution scratch
+  int32_t* perm_scratch = nullptr;  // Fisher-Yates resolution scratch (perm_scratch_ints)
+  int64_t perm_scratch_n = 0;       // its size in int32
   int dev_slot = 0;
   hipStream_t copy_stream = nullptr;  // H2D permutation uploads, overlapped with prepare()
   hipEvent_t perms_ready = nullptr;   // upload of the current learn's permutations done
@@ -668,13 +669,13 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
     // positions (the whole permutation is never resolved; perms_dev holds the marks)
     Timed tm(h, K_PERM, s);
     DPPO_TRY(launch_shard_select_targets(h->targets_dev2[ds], h->perms_dev, h->perm_scratch,
-                                         h->perms_local, h->seg, h->sel_cnt, h->Bg,
+                                         h->perm_scratch_n, h->perms_local, h->seg, h->sel_cnt, h->Bg,
                                          d.num_envs * h->nranks, d.num_envs * h->rank,
                                          d.num_envs, (int32_t)E, (int32_t)M, s));
   } else if (targets) {
     Timed tm(h, K_PERM, s);
     DPPO_TRY(launch_perm_resolve(h->targets_dev2[ds], h->perms_dev, h->pe, (int32_t)E,
-                                 h->perm_scratch, s));
+                                 h->perm_scratch, h->perm_scratch_n, s));
   }
   if (h->gmb && !(targets && perm_walk())) {
     // this rank's members of every global minibatch, in permutation order
@@ -908,7 +909,8 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
     chk(dalloc(&h->targets_dev2[k], E * h->pe));
   }
   h->perms_dev = h->perms_dev2[0];
-  chk(dalloc(&h->perm_scratch, 3 * E * h->pe));
+  h->perm_scratch_n = perm_scratch_ints(h->pe, (int32_t)E);
+  chk(dalloc(&h->perm_scratch, h->perm_scratch_n));
   if (h->gmb) {
     chk(dalloc(&h->perms_local, E * h->B));
     chk(dalloc(&h->seg, E * (M + 1)));
@@ -1277,12 +1279,13 @@ int dppo_global_minibatch_lists(dppo_handle* h, const int32_t* targets, int32_t*
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   Timed tm(h, K_PERM, S(stream));
   if (perm_walk())
-    return launch_shard_select_targets(targets, h->perms_dev, h->perm_scratch, local, seg,
+    return launch_shard_select_targets(targets, h->perms_dev, h->perm_scratch, h->perm_scratch_n,
+                                       local, seg,
                                        h->sel_cnt, h->Bg, d.num_envs * d.world_size,
                                        d.num_envs * d.rank, d.num_envs, d.num_epochs,
                                        d.num_minibatches, S(stream));
   DPPO_TRY(launch_perm_resolve(targets, h->perms_dev, h->Bg, d.num_epochs, h->perm_scratch,
-                               S(stream)));
+                               h->perm_scratch_n, S(stream)));
   return launch_shard_select(h->perms_dev, local, seg, h->sel_cnt, h->Bg,
                              d.num_envs * d.world_size, d.num_envs * d.rank, d.num_envs,
                              d.num_epochs, d.num_minibatches, S(stream));
@@ -1294,7 +1297,8 @@ int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t
     set_error("invalid argument to dppo_perm_resolve");
     return DPPO_EINVAL;
   }
-  return launch_perm_resolve(targets, perms, n, count, scratch, S(stream));
+  return launch_perm_resolve(targets, perms, n, count, scratch, 3 * n * (int64_t)count,
+                             S(stream));
 }
 
 int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out) {

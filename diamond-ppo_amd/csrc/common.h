@@ -402,10 +402,12 @@ int launch_gru_grad(const GruOffsets& po, const float* params, const dppo_gru_ba
                     int A, float inv_m, float clip_eps, float vf, float ent, const GruScratch& sc,
                     float* slabs, int64_t slab_stride, int64_t p_total, hipStream_t s);
 
-// Fisher-Yates resolution (shuffle.hip): perms[c][n] from swap targets[c][n];
-// scratch = 3 * count * n int32.
+// Fisher-Yates resolution (shuffle.hip): perms[c][n] from swap targets[c][n]; scratch of
+// scratch_ints >= 3 * count * n int32 (perm_scratch_ints: the size at which the partitioned
+// buckets run fused).
+int64_t perm_scratch_ints(int64_t n, int32_t count);
 int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
-                        int32_t* scratch, hipStream_t s);
+                        int32_t* scratch, int64_t scratch_ints, hipStream_t s);
 
 // Global-minibatch data parallelism (shuffle.hip): from E global permutations gperm[E][T*Ng]
 // keep, in order, the samples of env shard [env0, env0 + Nl) as local indices t*Nl + (n - env0)
@@ -416,8 +418,9 @@ int launch_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32
 // resolve + select instead (A/B).
 bool perm_walk();
 int launch_shard_select_targets(const int32_t* targets, int32_t* marks, int32_t* scratch,
-                                int32_t* local, int32_t* seg, int32_t* cnt, int64_t bg, int32_t ng,
-                                int32_t env0, int32_t nl, int32_t E, int32_t M, hipStream_t s);
+                                int64_t scratch_ints, int32_t* local, int32_t* seg, int32_t* cnt,
+                                int64_t bg, int32_t ng, int32_t env0, int32_t nl, int32_t E,
+                                int32_t M, hipStream_t s);
 int shard_select_chunks(int64_t bg);
 int launch_shard_select(const int32_t* gperm, int32_t* local, int32_t* seg, int32_t* cnt,
                         int64_t bg, int32_t ng, int32_t env0, int32_t nl, int32_t E, int32_t M,

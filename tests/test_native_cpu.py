@@ -398,3 +398,94 @@ def test_bench_refuses_a_world_that_differs_from_gpus():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "64"], env=env, cwd=ROOT,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 2 and "GPU(s) visible" in r.stderr, r.stderr[-2000:]
+
+
+def partitioned_bucket_shuffle(j, logp=2, chunk=8):
+    """NumPy restatement of the partitioned-bucket resolution (csrc/shuffle.hip csr_*): the steps
+    counted per chunk and target partition (count), prefixed over chunks (colscan) and partitions
+    (basescan), scattered to their partition's range (scatter, any order within it), sorted by
+    position inside the partition (fill: buckets contiguous, any order within a bucket), then
+    M(q) = min of bucket q above q (index) and out[i] = W(next larger step of i's bucket) or j_i
+    (solve).  Also returns the bucket starts the value walk reads (index, WALK)."""
+    n = len(j)
+    P = 1 << logp
+    nparts = (n + P - 1) // P
+    nchunks = (n + chunk - 1) // chunk
+    valid = [i for i in range(1, n) if 0 <= j[i] <= i]
+    hist = np.zeros((nchunks, nparts), np.int64)
+    for i in valid:
+        hist[i // chunk, j[i] >> logp] += 1
+    colpre = np.cumsum(hist, axis=0) - hist                  # colscan (exclusive over chunks)
+    tot = hist.sum(axis=0)
+    base = np.concatenate([[0], np.cumsum(tot)])             # basescan
+    cur = base[:-1][None, :] + colpre
+    pid = np.empty(len(valid), np.int64)
+    ppos = np.empty(len(valid), np.int64)
+    rng = np.random.default_rng(n)
+    for i in rng.permutation(valid) if valid else []:         # slots in arbitrary order
+        x = j[i] >> logp
+        k = i // chunk
+        slot = cur[k, x]
+        cur[k, x] += 1
+        pid[slot], ppos[slot] = i, j[i] & (P - 1)
+    ent = np.empty(len(valid), np.int64)
+    off = np.zeros(n + 1, np.int64)
+    for x in range(nparts):                                   # fill + index (bucket starts)
+        b0, b1 = base[x], base[x + 1]
+        cnt = np.bincount(ppos[b0:b1], minlength=P)
+        st = np.cumsum(cnt) - cnt
+        order = rng.permutation(np.arange(b0, b1))
+        c2 = st.copy()
+        for e in order:
+            ent[b0 + c2[ppos[e]]] = pid[e]
+            c2[ppos[e]] += 1
+        for p in range(P):
+            q = x * P + p
+            if q < n:
+                off[q] = b0 + st[p]
+                if q == n - 1:
+                    off[n] = b0 + st[p] + cnt[p]
+    bucket = [ent[off[q]:off[q + 1]] for q in range(n)]
+    M = np.array([min([i for i in b if i > q], default=-1) for q, b in enumerate(bucket)])
+
+    def root(q):
+        while M[q] >= 0:
+            q = M[q]
+        return q
+    out = np.array(j, np.int64).copy()                         # invalid steps pass through
+    out[0] = root(0)
+    for q, b in enumerate(bucket):                            # solve, bucket by bucket
+        for i in b:
+            nx = min([v for v in b if v > i], default=-1)
+            out[i] = root(nx) if nx >= 0 else q
+    return out, ent, off
+
+
+def test_partitioned_buckets_reproduce_the_shuffle():
+    """The partitioned-bucket passes (tiny partitions and chunks, so that every boundary is
+    crossed) give the sequential Fisher-Yates loop's permutation on all-zero, identity, shifted and
+    random targets, and their buckets drive the value walk to the inverse permutation."""
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 5, 17, 64, 300):
+        cases = [np.zeros(n, np.int64), np.arange(n), np.maximum(np.arange(n) - 1, 0),
+                 np.array([0] + [rng.integers(0, i + 1) for i in range(1, n)])]
+        for jj in cases:
+            a = fisher_yates(jj)
+            for logp, chunk in ((0, 1), (2, 8), (3, 5)):
+                out, ent, off = partitioned_bucket_shuffle(jj, logp, chunk)
+                assert np.array_equal(out, a), (n, logp, chunk)
+                inv = np.empty(n, np.int64)
+                inv[a] = np.arange(n)
+                for v in range(n):                            # walk_pos_csr
+                    q, bound = v, n
+                    while True:
+                        b = ent[off[q]:off[q + 1]]
+                        best = max([i for i in b if q < i < bound], default=-1)
+                        if best >= 0 or q == 0:
+                            pos = max(best, 0)
+                            break
+                        if jj[q] >= q:
+                            pos = q
+                            break
+                        bound, q = q, int(jj[q])
+                    assert pos == inv[v]
