@@ -460,16 +460,29 @@ __device__ void csr_ranges(const Pairs& pr, int64_t b0, int64_t b1, int P, int32
   __syncthreads();
 }
 
-// fill: the partition's step ids into ent[], bucket by bucket
+// fill: the partition's step ids into ent[], bucket by bucket; off (if given: the value walk on
+// the packed layout) = the bucket starts, as csr_index_kernel<true> writes them
 __global__ __launch_bounds__(kBlock) void csr_fill_kernel(Pairs pr,
                                                          const int32_t* __restrict__ base,
-                                                         int32_t* __restrict__ ent, int logp) {
+                                                         int32_t* __restrict__ ent,
+                                                         int32_t* __restrict__ off, int64_t n,
+                                                         int logp, int nparts) {
   extern __shared__ int32_t s[];  // cnt[P], cur[P]
   __shared__ int32_t ws[kBlock / 64];
   const int P = 1 << logp;
-  const int64_t b0 = base[blockIdx.x], b1 = base[blockIdx.x + 1];
+  const int64_t g = blockIdx.x, c = g / nparts, x = g - c * nparts;
+  const int64_t b0 = base[g], b1 = base[g + 1];
   csr_ranges(pr, b0, b1, P, s, s + P, ws);
   int32_t* cur = s + P;
+  if (off) {
+    for (int p = threadIdx.x; p < P; p += kBlock) {
+      const int64_t q = x * P + p;
+      if (q >= n) break;
+      off[c * (n + 1) + q] = (int32_t)(b0 + cur[p]);
+      if (q == n - 1) off[c * (n + 1) + n] = (int32_t)(b0 + cur[p] + s[p]);
+    }
+    __syncthreads();  // every start read before the fill moves cur
+  }
   for (int64_t e = b0 + threadIdx.x; e < b1; e += kBlock) {
     int32_t i, p;
     pr.get(e, i, p);
@@ -719,7 +732,7 @@ int csr_buckets(const CsrPlan& P, const int32_t* tgt, int32_t* scratch, int32_t*
   DPPO_LAUNCH_CHECK();
   if (!fill) return DPPO_OK;
   DPPO_LAUNCH(csr_fill_kernel, dim3(nb), dim3(kBlock), lds_fill, s, pr, base, scratch + P.r_ent,
-              P.logp);
+              P.pack ? scratch + P.r_dst : nullptr, n, P.logp, P.nparts);
   DPPO_LAUNCH_CHECK();
   return DPPO_OK;
 }
@@ -739,9 +752,11 @@ int csr_resolve(const CsrPlan& P, const int32_t* tgt, int32_t* perms, int32_t* s
   const unsigned nb = (unsigned)P.np;
   const size_t lds = 2 * ((size_t)1 << P.logp) * sizeof(int32_t);
   if (walk) {
-    DPPO_LAUNCH(csr_index_kernel<true>, dim3(nb), dim3(kBlock), lds, s, pr, base, ent, dst,
-                nullptr, n, P.logp, P.nparts);
-    DPPO_LAUNCH_CHECK();
+    if (!P.pack) {  // (packed: the fill wrote the bucket starts)
+      DPPO_LAUNCH(csr_index_kernel<true>, dim3(nb), dim3(kBlock), lds, s, pr, base, ent, dst,
+                  nullptr, n, P.logp, P.nparts);
+      DPPO_LAUNCH_CHECK();
+    }
     DPPO_LAUNCH(csr_walk_scatter_kernel, dim3(fy_grid(n * count)), dim3(kBlock), 0, s, tgt, ent,
                 dst, perms, n, n * count);
     DPPO_LAUNCH_CHECK();
@@ -879,10 +894,12 @@ int launch_shard_select_targets(const int32_t* targets, int32_t* marks, int32_t*
     const int rc = csr_buckets(P, targets, scratch, nullptr, bg, E, true, s);
     if (rc != DPPO_OK) return rc;
     int32_t* off = scratch + P.r_dst;
-    DPPO_LAUNCH(csr_index_kernel<true>, dim3((unsigned)P.np), dim3(kBlock),
-                2 * ((size_t)1 << P.logp) * sizeof(int32_t), s, csr_pairs(P, scratch),
-                scratch + P.r_base, scratch + P.r_ent, off, nullptr, bg, P.logp, P.nparts);
-    DPPO_LAUNCH_CHECK();
+    if (!P.pack) {  // (packed: the fill wrote the bucket starts)
+      DPPO_LAUNCH(csr_index_kernel<true>, dim3((unsigned)P.np), dim3(kBlock),
+                  2 * ((size_t)1 << P.logp) * sizeof(int32_t), s, csr_pairs(P, scratch),
+                  scratch + P.r_base, scratch + P.r_ent, off, nullptr, bg, P.logp, P.nparts);
+      DPPO_LAUNCH_CHECK();
+    }
     DPPO_LAUNCH(csr_walk_mark_kernel, dim3(fy_grid(b_local * E)), dim3(kBlock), 0, s, targets,
                 scratch + P.r_ent, off, marks, bg, b_local, E, ng, env0, nl);
     DPPO_LAUNCH_CHECK();

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Packed walk path (fill writes the bucket starts): correctness of the walk resolution and the
+# global lists, then the member lists at world 2 / 4 / 8.
+set -o pipefail
+O=gpurun_out/csr5; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dataparallel.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -k "fisher_yates or swap_targets or c5_full_size or global" > $O/pytest.log 2>&1
+rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python3 -c "
+import sys; sys.path.insert(0, 'tools'); import gmb_cap as g
+print('partitioned buckets: global lists ms', {w: round(g.global_lists_ms(w), 3) for w in (2, 4, 8)})
+" 2>&1 | grep -v amdgpu.ids
