@@ -313,7 +313,8 @@ int dppo_perm_par_stats(int64_t* out3);
 
 /* The swap half on the device: perms[c] = arange(n) shuffled by targets[c] (device int32
  * [count][n]), identical to the sequential Fisher-Yates loop.  scratch: device int32
- * [3 * count * n].  Stream-ordered. */
+ * [3 * count * n].  Stream-ordered.  (A handle's own resolution, dppo_learn_targets_f32, uses a
+ * larger internal scratch that lets its bucket sort store one packed word per step.) */
 int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
                       int32_t* scratch, void* stream);
 
