@@ -433,15 +433,16 @@ __global__ __launch_bounds__(kBlock) void csr_scatter_kernel(
 }
 
 // Bucket ranges of partition g in LDS: cnt[p] = its entries targeting position x * P + p,
-// st[p] = their start in the partition's sorted range (exclusive prefix of cnt)
+// st[p] = their start in the partition's sorted range (exclusive prefix of cnt); NT threads
+template <int NT = kBlock>
 __device__ void csr_ranges(const Pairs& pr, int64_t b0, int64_t b1, int P, int32_t* cnt,
                            int32_t* st, int32_t* ws) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int p = tid; p < P; p += kBlock) cnt[p] = 0;
+  for (int p = tid; p < P; p += NT) cnt[p] = 0;
   __syncthreads();
-  for (int64_t e = b0 + tid; e < b1; e += kBlock) atomicAdd(&cnt[pr.pos_of(e)], 1);
+  for (int64_t e = b0 + tid; e < b1; e += NT) atomicAdd(&cnt[pr.pos_of(e)], 1);
   __syncthreads();
-  const int per = P / kBlock;
+  const int per = P / NT;
   int32_t s = 0;
   for (int j = 0; j < per; ++j) s += cnt[tid * per + j];
   int32_t inc = s;
@@ -495,19 +496,22 @@ __global__ __launch_bounds__(kBlock) void csr_fill_kernel(Pairs pr,
 // -- into its range of ent instead, which this block then reads back from its own cache), then
 // per position q: M(q) = min{i > q in bucket q} into mq, and for every step v of the bucket
 // succ(v) = the next larger step of the bucket into succ (fy_solve_kernel's input)
+constexpr int kFillBlock = 1024;  // fill + index: 16 waves a workgroup (its 64 KB of LDS allow
+                                  // two workgroups per CU: 32 waves to hide the pair reads)
+
 template <bool LDS>
 __device__ __forceinline__ void csr_fill_index_body(const Pairs& pr, int64_t b0, int64_t b1,
                                                     int32_t* __restrict__ el, const int32_t* cnt,
                                                     int32_t* cur, int32_t* __restrict__ mq,
                                                     int32_t* __restrict__ succ, int64_t n,
                                                     int64_t c, int64_t x, int P) {
-  for (int64_t e = b0 + threadIdx.x; e < b1; e += kBlock) {
+  for (int64_t e = b0 + threadIdx.x; e < b1; e += kFillBlock) {
     int32_t i, p;
     pr.get(e, i, p);
     el[atomicAdd(&cur[p], 1)] = i;
   }
   __syncthreads();  // cur[p] is now the end of bucket p
-  for (int p = threadIdx.x; p < P; p += kBlock) {
+  for (int p = threadIdx.x; p < P; p += kFillBlock) {
     const int64_t q = x * P + p;
     if (q >= n) break;
     const int32_t k1 = cur[p], k0 = k1 - cnt[p];
@@ -526,16 +530,16 @@ __device__ __forceinline__ void csr_fill_index_body(const Pairs& pr, int64_t b0,
   }
 }
 
-__global__ __launch_bounds__(kBlock) void csr_fill_index_kernel(
+__global__ __launch_bounds__(kFillBlock) void csr_fill_index_kernel(
     Pairs pr, const int32_t* __restrict__ base, int32_t* __restrict__ ent,
     int32_t* __restrict__ mq, int32_t* __restrict__ succ, int64_t n, int logp, int nparts,
     int cap) {
   extern __shared__ int32_t s[];  // cnt[P], cur[P], the partition's buckets [cap]
-  __shared__ int32_t ws[kBlock / 64];
+  __shared__ int32_t ws[kFillBlock / 64];
   const int P = 1 << logp;
   const int64_t g = blockIdx.x, c = g / nparts, x = g - c * nparts;
   const int64_t b0 = base[g], b1 = base[g + 1];
-  csr_ranges(pr, b0, b1, P, s, s + P, ws);
+  csr_ranges<kFillBlock>(pr, b0, b1, P, s, s + P, ws);
   if (b1 - b0 <= cap)
     csr_fill_index_body<true>(pr, b0, b1, s + 2 * P, s, s + P, mq, succ, n, c, x, P);
   else
@@ -767,7 +771,7 @@ int csr_resolve(const CsrPlan& P, const int32_t* tgt, int32_t* perms, int32_t* s
     // partition sorts them into its own range of ent)
     const size_t lds_max = 65536 - 64;  // (the kernel's static wave sums)
     const int cap = (int)(lds_max / sizeof(int32_t)) - (2 << P.logp);
-    DPPO_LAUNCH(csr_fill_index_kernel, dim3(nb), dim3(kBlock), lds_max, s, pr, base, ent, dst,
+    DPPO_LAUNCH(csr_fill_index_kernel, dim3(nb), dim3(kFillBlock), lds_max, s, pr, base, ent, dst,
                 perms, n, P.logp, P.nparts, cap);
     DPPO_LAUNCH_CHECK();
   } else {
