@@ -1301,6 +1301,21 @@ int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t
                              S(stream));
 }
 
+int64_t dppo_perm_resolve_scratch(int64_t n, int32_t count) {
+  if (n < 0 || n > 0x7FFFFFFF || count < 0) return -1;
+  return perm_scratch_ints(n, count);
+}
+
+int dppo_perm_resolve_ex(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
+                         int32_t* scratch, int64_t scratch_ints, void* stream) {
+  if (!targets || !perms || !scratch || n < 0 || n > 0x7FFFFFFF || count < 0 ||
+      scratch_ints < 3 * n * (int64_t)count) {
+    set_error("invalid argument to dppo_perm_resolve_ex (scratch_ints < 3 * count * n?)");
+    return DPPO_EINVAL;
+  }
+  return launch_perm_resolve(targets, perms, n, count, scratch, scratch_ints, S(stream));
+}
+
 int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out) {
   if (!h || !out || slot < 0 || slot >= kPermSlots) {
     set_error("invalid argument to dppo_perm_buffer");

@@ -496,6 +496,50 @@ __global__ __launch_bounds__(kBlock) void csr_fill_kernel(Pairs pr,
 // -- into its range of ent instead, which this block then reads back from its own cache), then
 // per position q: M(q) = min{i > q in bucket q} into mq, and for every step v of the bucket
 // succ(v) = the next larger step of the bucket into succ (fy_solve_kernel's input)
+// M(q) and succ(v) for every step v of bucket q = b[0 .. m) (in LDS or memory; the steps are
+// distinct and >= q).  Small buckets by a min scan per step (what random targets give: ~ln(n/q)
+// steps); a larger one -- adversarial but valid targets, e.g. every j_i = 0, one bucket of n - 1
+// steps -- is heap-sorted in place first, O(m log m) in this thread instead of O(m^2).  succ is
+// the epoch's base; returns M(q) (-1: none).
+__device__ __forceinline__ int32_t csr_bucket_links(int32_t* __restrict__ b, int32_t m, int64_t q,
+                                                    int32_t* __restrict__ succ) {
+  if (m <= 32) {
+    int32_t mq = 0x7FFFFFFF;
+    for (int32_t k = 0; k < m; ++k) {
+      const int32_t v = b[k];
+      mq = (v > q && v < mq) ? v : mq;
+      int32_t nx = 0x7FFFFFFF;
+      for (int32_t f = 0; f < m; ++f) {
+        const int32_t w = b[f];
+        nx = (w > v && w < nx) ? w : nx;
+      }
+      succ[v] = nx == 0x7FFFFFFF ? -1 : nx;
+    }
+    return mq == 0x7FFFFFFF ? -1 : mq;
+  }
+  auto sift = [&](int32_t r, int32_t end) {
+    for (;;) {
+      int32_t ch = 2 * r + 1;
+      if (ch >= end) break;
+      if (ch + 1 < end && b[ch + 1] > b[ch]) ++ch;
+      if (b[r] >= b[ch]) break;
+      const int32_t t = b[r];
+      b[r] = b[ch];
+      b[ch] = t;
+      r = ch;
+    }
+  };
+  for (int32_t r = m / 2 - 1; r >= 0; --r) sift(r, m);
+  for (int32_t end = m - 1; end > 0; --end) {
+    const int32_t t = b[0];
+    b[0] = b[end];
+    b[end] = t;
+    sift(0, end);
+  }
+  for (int32_t k = 0; k < m; ++k) succ[b[k]] = k + 1 < m ? b[k + 1] : -1;
+  return b[0] > q ? b[0] : (m > 1 ? b[1] : -1);
+}
+
 constexpr int kFillBlock = 1024;  // fill + index: 16 waves a workgroup (its 64 KB of LDS allow
                                   // two workgroups per CU: 32 waves to hide the pair reads)
 
@@ -515,18 +559,7 @@ __device__ __forceinline__ void csr_fill_index_body(const Pairs& pr, int64_t b0,
     const int64_t q = x * P + p;
     if (q >= n) break;
     const int32_t k1 = cur[p], k0 = k1 - cnt[p];
-    int32_t m = 0x7FFFFFFF;
-    for (int32_t k = k0; k < k1; ++k) {
-      const int32_t v = el[k];
-      m = (v > q && v < m) ? v : m;
-      int32_t nx = 0x7FFFFFFF;
-      for (int32_t f = k0; f < k1; ++f) {
-        const int32_t w = el[f];
-        nx = (w > v && w < nx) ? w : nx;
-      }
-      succ[c * n + v] = nx == 0x7FFFFFFF ? -1 : nx;
-    }
-    mq[c * n + q] = m == 0x7FFFFFFF ? -1 : m;
+    mq[c * n + q] = csr_bucket_links(el + k0, k1 - k0, q, succ + c * n);
   }
 }
 
@@ -551,7 +584,7 @@ __global__ __launch_bounds__(kFillBlock) void csr_fill_index_kernel(
 template <bool WALK>
 __global__ __launch_bounds__(kBlock) void csr_index_kernel(Pairs pr,
                                                           const int32_t* __restrict__ base,
-                                                          const int32_t* __restrict__ ent,
+                                                          int32_t* __restrict__ ent,
                                                           int32_t* __restrict__ dst,
                                                           int32_t* __restrict__ succ, int64_t n,
                                                           int logp, int nparts) {
@@ -569,19 +602,8 @@ __global__ __launch_bounds__(kBlock) void csr_index_kernel(Pairs pr,
       dst[c * (n + 1) + q] = (int32_t)e0;
       if (q == n - 1) dst[c * (n + 1) + n] = (int32_t)e1;
     } else {
-      int32_t m = 0x7FFFFFFF;
-      for (int64_t e = e0; e < e1; ++e) {
-        const int32_t v = ent[e];
-        m = (v > q && v < m) ? v : m;
-        // succ(v) = the next larger step of the bucket (fy_solve_kernel's input, read from out)
-        int32_t nx = 0x7FFFFFFF;
-        for (int64_t f = e0; f < e1; ++f) {
-          const int32_t w = ent[f];
-          nx = (w > v && w < nx) ? w : nx;
-        }
-        succ[c * n + v] = nx == 0x7FFFFFFF ? -1 : nx;
-      }
-      dst[c * n + q] = m == 0x7FFFFFFF ? -1 : m;
+      // (succ: fy_solve_kernel's input, read from out)
+      dst[c * n + q] = csr_bucket_links(ent + e0, (int32_t)(e1 - e0), q, succ + c * n);
     }
   }
 }

@@ -32,7 +32,7 @@ EXPORTED = [
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_perm_external", "dppo_perm_external_done", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_global_minibatch_lists", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
+    "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_perm_resolve_scratch", "dppo_perm_resolve_ex", "dppo_global_minibatch_lists", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
     "dppo_peer_export", "dppo_peer_open", "dppo_peer_close", "dppo_peer_allreduce", "dppo_peer_info",
     "dppo_peer_selftest",
@@ -143,6 +143,8 @@ def load():
         "dppo_perm_wait": (ctypes.c_int, [vp]),
         "dppo_perm_stats": (ctypes.c_int, [P(i64)]),
         "dppo_perm_resolve": (ctypes.c_int, [vp, vp, i64, i32, vp, vp]),
+        "dppo_perm_resolve_scratch": (i64, [i64, i32]),
+        "dppo_perm_resolve_ex": (ctypes.c_int, [vp, vp, i64, i32, vp, i64, vp]),
         "dppo_global_minibatch_lists": (ctypes.c_int, [vp, vp, vp, vp, vp]),
         "dppo_comm_unique_id": (ctypes.c_int, [vp]),
         "dppo_comm_init": (ctypes.c_int, [vp, i32, i32, vp]),
@@ -310,6 +312,18 @@ def perm_resolve(targets_dev: int, perms_dev: int, n: int, count: int, scratch_d
     targets[c]; scratch holds 3*count*n int32."""
     check(load().dppo_perm_resolve(targets_dev, perms_dev, int(n), int(count), scratch_dev,
                                    stream), "dppo_perm_resolve")
+
+
+def perm_resolve_scratch(n: int, count: int) -> int:
+    """int32 scratch elements at which dppo_perm_resolve_ex runs its packed, fused form."""
+    return int(load().dppo_perm_resolve_scratch(int(n), int(count)))
+
+
+def perm_resolve_ex(targets_dev: int, perms_dev: int, n: int, count: int, scratch_dev: int,
+                    scratch_ints: int, stream: int):
+    """dppo_perm_resolve with an explicit scratch size (>= 3*count*n int32)."""
+    check(load().dppo_perm_resolve_ex(targets_dev, perms_dev, int(n), int(count), scratch_dev,
+                                      int(scratch_ints), stream), "dppo_perm_resolve_ex")
 
 
 class Handle:

@@ -317,6 +317,13 @@ int dppo_perm_par_stats(int64_t* out3);
  * larger internal scratch that lets its bucket sort store one packed word per step.) */
 int dppo_perm_resolve(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
                       int32_t* scratch, void* stream);
+/* dppo_perm_resolve with the scratch size given (int32 elements, >= 3 * count * n): from
+ * dppo_perm_resolve_scratch(n, count) up, the bucket sort stores one packed word per step and
+ * fuses its bucket pass in LDS (the handle's own form; ~1.8x faster at 4 x 8.4 M).  Same results
+ * bit for bit.  dppo_perm_resolve_scratch returns -1 on invalid sizes. */
+int64_t dppo_perm_resolve_scratch(int64_t n, int32_t count);
+int dppo_perm_resolve_ex(const int32_t* targets, int32_t* perms, int64_t n, int32_t count,
+                         int32_t* scratch, int64_t scratch_ints, void* stream);
 
 /* Global minibatches on the device (dims.global_minibatches, world_size > 1): from the swap
  * targets of the GLOBAL batch (device int32 [E][T*N*world_size], dppo_perm_targets_numpy of

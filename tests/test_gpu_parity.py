@@ -447,6 +447,58 @@ def test_device_fisher_yates_resolution_matches_numpy(monkeypatch, walk, n, coun
     assert np.array_equal(out.cpu().numpy(), ref)
 
 
+def _fisher_yates(j):
+    a = np.arange(len(j), dtype=np.int32)
+    for i in range(len(j) - 1, 0, -1):
+        k = int(j[i])
+        a[i], a[k] = a[k], a[i]
+    return a
+
+
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("n,count", [(1000, 4), (65539, 2), (524288, 4)])
+def test_device_resolution_packed_and_public_scratch_match_numpy(monkeypatch, packed, n, count):
+    """dppo_perm_resolve_ex with the packed-pair scratch (dppo_perm_resolve_scratch: the handle's
+    own form) and with the public 3 * count * n: both equal np.random.permutation, bit-exact."""
+    monkeypatch.setenv("DPPO_PERM_WALK", "0")
+    np.random.seed(2000 + n)
+    key, pos, _ = N.mt_state()
+    tg = np.empty(count * n, np.int32)
+    N.perm_targets_numpy(key, pos, n, count, tg)
+    np.random.seed(2000 + n)
+    ref = np.concatenate([np.random.permutation(n) for _ in range(count)]).astype(np.int32)
+    ints = N.perm_resolve_scratch(n, count) if packed else 3 * count * n
+    assert ints >= 3 * count * n
+    out = torch.full((count * n,), -7, dtype=torch.int32, device=dev())
+    scratch = torch.empty(ints, dtype=torch.int32, device=dev())
+    N.perm_resolve_ex(t(tg, torch.int32).data_ptr(), out.data_ptr(), n, count, scratch.data_ptr(),
+                      ints, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("packed", [False, True])
+@pytest.mark.parametrize("kind", ["zeros", "identity", "shifted"])
+def test_device_resolution_on_adversarial_targets(monkeypatch, packed, kind):
+    """Valid but adversarial swap targets (every j_i <= i is a Fisher-Yates input): all zero -- one
+    bucket of n - 1 steps, sorted in place in O(m log m) --, identity, shifted; the sequential
+    loop's permutation, bit-exact, on both scratch forms and within the test's time limit."""
+    monkeypatch.setenv("DPPO_PERM_WALK", "0")
+    n, count = 65539, 2
+    i = np.arange(n)
+    j = {"zeros": np.zeros(n), "identity": i, "shifted": np.maximum(i - 1, 0)}[kind].astype(np.int32)
+    tg = np.concatenate([j] * count)
+    ref = np.concatenate([_fisher_yates(j)] * count)
+    ints = N.perm_resolve_scratch(n, count) if packed else 3 * count * n
+    out = torch.full((count * n,), -7, dtype=torch.int32, device=dev())
+    scratch = torch.empty(ints, dtype=torch.int32, device=dev())
+    N.perm_resolve_ex(t(tg, torch.int32).data_ptr(), out.data_ptr(), n, count, scratch.data_ptr(),
+                      ints, stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("device_shuffle", [False, True])
 def test_permutation_lookahead_hit_and_miss(device_shuffle):
     """The next learn's permutations are drawn ahead on a host thread; they are used only while

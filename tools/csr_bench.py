@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--walk", default="0")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--public", action="store_true",
+                    help="the public 3 * count * n scratch (default: dppo_perm_resolve_scratch)")
     a = ap.parse_args()
     os.environ["DPPO_PERM_WALK"] = a.walk
     n, count = a.n, a.count
@@ -33,18 +35,22 @@ def main():
     dev = torch.device("cuda:0")
     td = torch.from_numpy(tg).to(dev)
     out = torch.empty(count * n, dtype=torch.int32, device=dev)
-    scratch = torch.empty(3 * count * n, dtype=torch.int32, device=dev)
+    ints = 3 * count * n if a.public else N.perm_resolve_scratch(n, count)
+    scratch = torch.empty(ints, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
+    call = lambda: N.perm_resolve_ex(td.data_ptr(), out.data_ptr(), n, count, scratch.data_ptr(),
+                                     ints, st)
     for _ in range(3):
-        N.perm_resolve(td.data_ptr(), out.data_ptr(), n, count, scratch.data_ptr(), st)
+        call()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.reps):
-        N.perm_resolve(td.data_ptr(), out.data_ptr(), n, count, scratch.data_ptr(), st)
+        call()
     e1.record()
     torch.cuda.synchronize(dev)
-    res = {"n": n, "count": count, "walk": a.walk, "lib": os.environ.get("DPPO_LIB", "default"),
+    res = {"n": n, "count": count, "walk": a.walk, "scratch_ints": ints,
+           "lib": os.environ.get("DPPO_LIB", "default"),
            "ms_per_call": round(e0.elapsed_time(e1) / a.reps, 4)}
     if not a.no_check:
         np.random.seed(123)
