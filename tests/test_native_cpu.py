@@ -489,3 +489,19 @@ def test_partitioned_buckets_reproduce_the_shuffle():
                             break
                         bound, q = q, int(jj[q])
                     assert pos == inv[v]
+
+
+def test_perm_resolve_scratch_contract():
+    """dppo_perm_resolve_scratch (host-only arithmetic, no GPU): never below the public
+    3 * count * n; above it wherever the partitioned buckets apply (the packed pairs and the fused
+    bucket pass: ~4.1 x count * n, more for tiny n, whose regions are 256-B aligned), exactly
+    3 * count * n where they do not (n < 2); -1 on invalid sizes."""
+    from diamond import _native as N
+    for n, count in ((1, 1), (17, 2), (1000, 4), (65539, 2), (8388608, 4)):
+        s = N.perm_resolve_scratch(n, count)
+        assert s >= 3 * count * n, (n, count, s)
+    assert N.perm_resolve_scratch(1, 3) == 3 * 3 * 1
+    assert N.perm_resolve_scratch(17, 2) > 3 * 2 * 17
+    big = N.perm_resolve_scratch(8388608, 4)
+    assert 4 * 4 * 8388608 < big < 5 * 4 * 8388608
+    assert N.perm_resolve_scratch(-1, 4) == -1 and N.perm_resolve_scratch(8, -1) == -1
