@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the DPPO_ABL_CSR_* timing-only scatter variants it builds against lived in the
+# intermediate tree of that measurement, profiles/r05_perm_csr.txt, and are not kept in shuffle.hip)
 # Partitioned-bucket resolution alone (tools/csr_bench.py, configs[4] size): the default library
 # (checked bit-exact, both modes), the linked lists (DPPO_PERM_CSR=0), and the two timing-only
 # scatter ablations, each under rocprofv3 for the per-pass split.

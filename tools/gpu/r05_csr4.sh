@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the DPPO_ABL_CSR_* timing-only scatter variants it builds against lived in the
+# intermediate tree of that measurement, profiles/r05_perm_csr.txt, and are not kept in shuffle.hip)
 # Scatter store shape (timing-only, tools/csr_bench.py): step ids only, and one packed 8-B store,
 # against the shipped two-array scatter.
 set -o pipefail
