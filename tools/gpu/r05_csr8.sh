@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical: DPPO_PERM_CSR2, the two-level scatter it measured, is not kept in shuffle.hip)
 # Two-level scatter (DPPO_PERM_CSR2=1, opt-in): resolution / learn / global-list tests under it
 # (both walk modes), C5 A/B against the one-level scatter, the resolution microbench split, and
 # the world-8 member lists.
