@@ -148,6 +148,7 @@ struct dppo_handle {
   bool ext_pending[kExtSlots] = {};
   int32_t trace_rows = 0;
   hipStream_t last_stream = nullptr;
+  hipEvent_t order_ev = nullptr;  // orders a call on another stream after the last learn
   // optional per-kernel-class timing with HIP events on the launch stream
   bool timing = false;
   struct Rec {
@@ -283,23 +284,26 @@ inline hipStream_t S(void* s) { return (hipStream_t)s; }
 int device_status(const dppo_handle* h) {
   const unsigned e = h->err_host ? __atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) : 0u;
   if (e == 0u) return DPPO_OK;
-  if (e == kErrPeerTimeout) {
-    set_error("a peer exchange timed out: another rank did not reach the same all-reduce within "
-              "%.0f s (DPPO_PEER_TIMEOUT_S); that optimizer step used this rank's gradient alone "
-              "and this handle is no longer usable", (double)h->xticks / 1e8);
+  const unsigned code = e & 0xffu, rank = (e >> 8) & 0xffu, idx = e >> 16;
+  if (code == kErrPeerTimeout) {
+    set_error("a peer exchange timed out: rank %u's word %u (slice or gradient element) did not "
+              "arrive within %.0f s (DPPO_PEER_TIMEOUT_S) -- another rank did not reach the same "
+              "all-reduce, or its publish is not visible here; that optimizer step used this "
+              "rank's gradient alone and this handle is no longer usable",
+              rank, idx, (double)h->xticks / 1e8);
     return DPPO_ECOMM;
   }
-  if (e == kErrTagTimeout) {
-    set_error("the optimizer step's fan-in timed out (code 3: a block's tagged word never "
-              "arrived -- its workgroups were not all resident at once, or a block left early); "
+  if (code == kErrTagTimeout) {
+    set_error("the optimizer step's fan-in timed out (code 3: tagged word %u never arrived at "
+              "block %u -- its workgroups were not all resident at once, or a block left early); "
               "the parameters of that step were left unchanged and this handle is no longer "
-              "usable");
+              "usable", idx, rank);
     return DPPO_EHIP;
   }
-  set_error("a grid-wide fan-in timed out (code %u): its workgroups were not all resident on the "
-            "device at once (another process holding the CUs, or a partitioned device); the "
-            "parameters of that optimizer step were left unchanged and this handle is no longer "
-            "usable", e);
+  set_error("a grid-wide fan-in timed out (code %u, block %u): its workgroups were not all "
+            "resident on the device at once (another process holding the CUs, or a partitioned "
+            "device); the parameters of that optimizer step were left unchanged and this handle "
+            "is no longer usable", code, idx);
   return DPPO_EHIP;
 }
 
@@ -632,6 +636,19 @@ int upload_perms(dppo_handle* h, const int32_t* host, int32_t* dst, int ds) {
   return DPPO_OK;
 }
 
+// Calls that use the handle's workspace run after the previous such call even when the caller
+// switches streams (one extra event record + wait only then); the stream becomes the one the
+// next call follows.
+int order_after_last(dppo_handle* h, hipStream_t s) {
+  if (h->last_stream && h->last_stream != s) {
+    if (!h->order_ev) DPPO_HIP_CHECK(hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming));
+    DPPO_HIP_CHECK(hipEventRecord(h->order_ev, h->last_stream));
+    DPPO_HIP_CHECK(hipStreamWaitEvent(s, h->order_ev, 0));
+  }
+  h->last_stream = s;
+  return DPPO_OK;
+}
+
 int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float* adam_m,
                float* adam_v, const dppo_hparams* hp, const int32_t* host_buf, bool targets,
                const dppo_learn_outputs* outputs, void* stream) {
@@ -655,6 +672,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
   hipStream_t s = S(stream);
+  DPPO_TRY(order_after_last(h, s));
   const int64_t E = d.num_epochs, M = d.num_minibatches;
   // permutations (ppo.py:252-255): host -> pinned staging -> device on the copy stream, beside
   // prepare(); given as swap targets they are shuffled on the device after prepare()
@@ -1007,6 +1025,7 @@ void dppo_destroy(dppo_handle* h) {
     if (h->perms_free[k]) (void)hipEventDestroy(h->perms_free[k]);
   }
   if (h->perms_ready) (void)hipEventDestroy(h->perms_ready);
+  if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
   (void)hipFree(h->perm_scratch);
   (void)hipFree(h->perms_local);
@@ -1277,6 +1296,9 @@ int dppo_global_minibatch_lists(dppo_handle* h, const int32_t* targets, int32_t*
     return DPPO_EINVAL;
   }
   DPPO_HIP_CHECK(hipSetDevice(h->device));
+  // the lists are built in the handle's own workspace (perms_dev as marks, perm_scratch,
+  // sel_cnt), which a learn enqueued on another stream may still be reading
+  DPPO_TRY(order_after_last(h, S(stream)));
   Timed tm(h, K_PERM, S(stream));
   if (perm_walk())
     return launch_shard_select_targets(targets, h->perms_dev, h->perm_scratch, h->perm_scratch_n,
@@ -1606,7 +1628,7 @@ int dppo_peer_close(dppo_handle* h) {
   peer_unmap(h);
   // a failed exchange (e.g. the self-test) leaves nothing in flight after the synchronisation:
   // the handle is usable again on its other transport
-  if (h->err_host && __atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) == kErrPeerTimeout)
+  if (h->err_host && (__atomic_load_n(h->err_host, __ATOMIC_ACQUIRE) & 0xffu) == kErrPeerTimeout)
     __atomic_store_n(h->err_host, 0u, __ATOMIC_RELEASE);
   if (!h->comm) {
     h->nranks = h->dims.world_size;

@@ -165,11 +165,18 @@ __device__ __forceinline__ void write_trace(float* trace, float s_pi, float s_v,
 constexpr unsigned kErrFaninTimeout = 1u;  // a grid-wide fan-in gave up waiting: grid not resident
 constexpr unsigned kErrPeerTimeout = 2u;   // a peer exchange gave up waiting for another rank
 constexpr unsigned kErrTagTimeout = 3u;    // reduce_adam's tagged-word fan-in gave up waiting
-// A wait that runs out of time records its code only when the word is still clear, and a wait
-// that finds the word already set leaves without writing: the first cause is what the host reads.
+// The word: bits 0-7 the code, 8-15 a rank, 16-31 an index (block, word or slice) -- the wait
+// that gave up, so a host report names WHICH wait stalled, not only its kind.
+// A wait that runs out of time records its word only when the word is still clear (one
+// compare-and-swap), and a wait that finds the word already set leaves without writing: the
+// first cause is what the host reads.
+__device__ __forceinline__ unsigned err_word(unsigned code, unsigned rank, unsigned idx) {
+  return code | (rank & 0xffu) << 8 | (idx & 0xffffu) << 16;
+}
 __device__ __forceinline__ void raise_err(unsigned* err, unsigned code) {
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u)
-    __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned expect = 0u;  // one compare-and-swap: of two waves timing out together, the first wins
+  __hip_atomic_compare_exchange_strong(err, &expect, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ bool err_set(const unsigned* err) {
   return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
@@ -209,7 +216,7 @@ __device__ __forceinline__ bool grid_fanin(unsigned* ctr, unsigned epoch,
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks;
       if (late || err_set(err)) {
-        if (late) raise_err(err, kErrFaninTimeout);
+        if (late) raise_err(err, err_word(kErrFaninTimeout, 0u, blockIdx.x));
         return false;
       }
     }
@@ -365,7 +372,7 @@ __device__ __forceinline__ T peer_get(const T* p) {
 }
 // Wait until *f reaches a.seq (wrap-safe); false -- with kErrPeerTimeout raised -- after
 // a.timeout_ticks of wall clock or once the handle's error word is already set.
-__device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a) {
+__device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a, int r, int slot) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned k = 0;
        (int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.seq) < 0; ++k) {
@@ -373,7 +380,7 @@ __device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a) 
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
       if (late || err_set(a.err)) {
-        if (late) raise_err(a.err, kErrPeerTimeout);
+        if (late) raise_err(a.err, err_word(kErrPeerTimeout, (unsigned)r, (unsigned)slot));
         return false;
       }
     }

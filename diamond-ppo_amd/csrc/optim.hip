@@ -240,7 +240,13 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
       if ((k & 255u) == 255u) {
         const bool late = __builtin_amdgcn_s_memrealtime() - t0 > pl.timeout_ticks;
         if (late || err_set(err)) {
-          if (late) raise_err(err, kErrPeerTimeout);
+          if (late) {  // the first lane still waiting names the rank and the word
+            const unsigned long long b = __ballot(pend != 0);
+            const int l = __ffsll((long long)b) - 1;
+            const unsigned pr = (unsigned)__shfl((int)pend, l);
+            const unsigned r = (unsigned)(__ffs((int)pr) - 1);
+            if (lane == l) raise_err(err, err_word(kErrPeerTimeout, r, (unsigned)p));
+          }
           return;  // parameters untouched; the handle reports the error
         }
       }
@@ -281,9 +287,26 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     if (__ballot(pending != 0) == 0) break;
     __builtin_amdgcn_s_sleep(1);
     if ((k & 255u) == 255u) {
-      const bool late = __builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks;
+      // with a peer exchange in front, this wait's bound starts after the peer wait's has run
+      // out: a block stuck on a peer word then reports as a peer timeout (code 2 + rank + word)
+      // instead of its siblings reporting the tag wait it caused (round-5 diagnosis)
+      const bool late = __builtin_amdgcn_s_memrealtime() - t0 >
+                        timeout_ticks + (pl.world > 0 ? pl.timeout_ticks : 0ull);
       if (late || err_set(err)) {
-        if (late) raise_err(err, kErrTagTimeout);
+        if (late) {  // the first word still missing: the block index (or nb + loss slot)
+          unsigned first = 0xffffu;
+#pragma unroll
+          for (int j = kTagWordsPerLane - 1; j >= 0; --j)
+            if (pending & (1u << j)) first = (unsigned)(j * 64 + lane);
+          const unsigned long long b = __ballot(pending != 0);
+          unsigned lo = 0xffffu;
+          for (unsigned long long bb = b; bb; bb &= bb - 1) {
+            const int l = __ffsll((long long)bb) - 1;
+            const unsigned f = (unsigned)__shfl((int)first, l);
+            lo = f < lo ? f : lo;
+          }
+          if (lane == 0) raise_err(err, err_word(kErrTagTimeout, blockIdx.x & 0xffu, lo));
+        }
         return;  // parameters untouched; the next C-ABI call reports the error
       }
     }

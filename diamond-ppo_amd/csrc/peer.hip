@@ -60,7 +60,7 @@ __global__ __launch_bounds__(kPeerThreads) void peer_sum_kernel(PeerArgs a) {
   }
   __syncthreads();
   // thread r waits for rank r's flag of this slice
-  if ((int)threadIdx.x < a.world && !peer_wait(peer_flag(a, threadIdx.x, s), a)) failed = 1;
+  if ((int)threadIdx.x < a.world && !peer_wait(peer_flag(a, threadIdx.x, s), a, threadIdx.x, s)) failed = 1;
   __syncthreads();
   if (failed) return;  // the destination keeps the local vector; the handle reports the error
   // every load of the thread's elements in flight before the first add (one link latency, not

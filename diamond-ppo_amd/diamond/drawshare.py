@@ -19,9 +19,14 @@ Protocol (``SLOTS`` slots; draft ``j`` of a learner -- its j-th look-ahead draw 
 * follower: waits for the slot's generation to move past what it has released with the header's
   draft index equal to its own ``j``; takes the slot only if the fingerprint equals that of its
   OWN state (otherwise, or after ``DPPO_PERM_SHARE_TIMEOUT_S``, it draws itself: the result is
-  always the draw of its own state); releases a slot it used once its upload from it is done
-  (``dppo_perm_external_done``, polled at every learn), and any slot holding a draft index it
-  has passed.
+  always the draw of its own state).  A slot it took is HELD from ``follow()`` until its learn
+  has enqueued the upload (``used()``: held -> pending) or the draft is dropped unused
+  (``drop()``, a look-ahead miss); a pending slot is released once its upload is done
+  (``dppo_perm_external_done``, polled at every learn).  Only a slot holding a draft index it has
+  passed and never took (skipped: mismatch or timeout) is released on sight.
+
+The leader holds its own drafts the same way, so it never draws over a draft of its own that is
+still waiting for its learn.
 
 Every wait is bounded.  A leader that cannot get a slot back raises (a follower that stopped
 releasing is a follower that stopped learning).  Design notes: DESIGN.md §6.
@@ -103,6 +108,7 @@ class NodeDrawShare:
             self._registered.append(s)
         self.g[16 + self.me] = 1  # active
         self.pending = []         # (slot, generation) uploads in flight
+        self.held = {}            # slot -> generation: taken, upload not yet enqueued
         self._mu = threading.Lock()  # pump() runs on the launching and the draft thread
         self.j = 0                # this rank's next draft index
         self.live = 0             # the lowest draft index this rank may still take
@@ -129,8 +135,10 @@ class NodeDrawShare:
                 else:
                     still.append((s, gen))
             self.pending = still
-            busy = {s for s, _ in self.pending}
-        if not self.leader:
+            if self.leader:
+                return
+            # under the lock: follow() marks a slot held and moves `live` past it atomically
+            busy = {s for s, _ in self.pending} | set(self.held)
             for s in range(SLOTS):
                 h = self.hdr[s]
                 if (s not in busy and int(h[0]) > int(h[400 + self.me])
@@ -138,9 +146,20 @@ class NodeDrawShare:
                     h[400 + self.me] = int(h[0])
 
     def used(self, s: int, gen: int):
-        """The learn just enqueued uploads from slot ``s`` (content ``gen``)."""
+        """The learn just enqueued uploads from slot ``s`` (content ``gen``): held -> pending."""
         with self._mu:
+            self.held.pop(s, None)
             self.pending.append((s, gen))
+
+    def drop(self, s: int, gen: int):
+        """A draft taken from slot ``s`` (content ``gen``) will not be uploaded (look-ahead miss,
+        failed learn, shutdown): give the slot back at once."""
+        with self._mu:
+            if self.held.get(s) != gen:
+                return
+            del self.held[s]
+            if not self.leader:
+                self.hdr[s][400 + self.me] = max(gen, int(self.hdr[s][400 + self.me]))
 
     # -- leader -----------------------------------------------------------------------------
     def lead(self, key: np.ndarray, pos: int, draw) -> tuple[int, int, int]:
@@ -155,7 +174,7 @@ class NodeDrawShare:
         while True:
             self.pump()
             with self._mu:
-                own_done = all(ps != s for ps, _ in self.pending)
+                own_done = s not in self.held and all(ps != s for ps, _ in self.pending)
             free = all(self._released(s, r) >= gen for r in range(1, self.nloc)
                        if int(self.g[16 + r]) == 1)
             if own_done and free:
@@ -170,6 +189,8 @@ class NodeDrawShare:
         h[3] = pos_out
         h[2] = fp
         h[1] = j
+        with self._mu:
+            self.held[s] = gen + 1
         h[0] = gen + 1  # publish: every field above is already stored
         self.stats["shared"] += 1
         return s, gen + 1, pos_out
@@ -180,11 +201,13 @@ class NodeDrawShare:
         (slot, generation, key_out, pos_out); None -> draw it yourself."""
         j = self.j
         self.j += 1
-        self.live = j
+        with self._mu:
+            self.live = j
         try:
             return self._follow(j, key, pos)
         finally:
-            self.live = j + 1
+            with self._mu:
+                self.live = j + 1
 
     def _follow(self, j: int, key: np.ndarray, pos: int):
         s = j % SLOTS
@@ -202,6 +225,8 @@ class NodeDrawShare:
                     h[400 + self.me] = gen
                     self.stats["mismatch"] += 1
                     return None
+                with self._mu:  # held until used() or drop(): pump() must not release it
+                    self.held[s] = gen
                 self.stats["shared"] += 1
                 return s, gen, key_out, pos_out
             if int(h[1]) > j:  # the leader is past this draft: not for us

@@ -414,11 +414,14 @@ class NativeLearner:
         self.share = None
         self._cur_share = None
         d = torch.distributed
-        if (self.global_mb and self.device_shuffle and self.lookahead and not _SOLO[0]
-                and os.environ.get("DPPO_PERM_SHARE", "1") != "0"
-                and d.is_available() and d.is_initialized()):
-            from . import drawshare
-            self.share = drawshare.setup(d, self)
+        if not _SOLO[0] and d.is_available() and d.is_initialized():
+            # setup() is a collective: enter it on every rank or on none (the enable inputs are
+            # per-process environment and sizing, so the ranks agree on them first)
+            want = (self.global_mb and self.device_shuffle and self.lookahead
+                    and os.environ.get("DPPO_PERM_SHARE", "1") != "0")
+            if self._all_ranks(d, want):
+                from . import drawshare
+                self.share = drawshare.setup(d, self)
 
     def _init_comm(self):
         """The rank exchange of the data-parallel learn.  DPPO_COMM: "auto" (default) = an RCCL
@@ -647,10 +650,17 @@ class NativeLearner:
         if t is not None:
             N.perm_wait(t)
 
+    def _drop(self, d):
+        """A finished draft that will not be uploaded: give back the shared slot it holds."""
+        if d.get("share") is not None and self.share is not None:
+            self.share.drop(*d["share"])
+
     def _drain_drafts(self):
         """Wait for every queued draft (their slots are being written) and drop them."""
         while self._drafts:
-            self._finish(self._drafts.popleft())
+            d = self._drafts.popleft()
+            self._finish(d)
+            self._drop(d)
 
     def close(self):
         """Release the handle safely: first every queued draft and the host-pool swaps still
@@ -696,6 +706,7 @@ class NativeLearner:
                 return d["buf"], d["key_out"], d["pos_out"]
             # the RNG moved between learns (or a draft failed): every later draft is chained
             # on the wrong state
+            self._drop(d)
             self._drain_drafts()
         buf = self.handle.perm_buffer(self._slot)
         draw = N.perm_targets_numpy if self.device_shuffle else N.perm_numpy
@@ -732,12 +743,18 @@ class NativeLearner:
             hp = hparams(cfg, lr, step0)
             fn = (self.handle.lib.dppo_learn_targets_f32 if self.device_shuffle
                   else self.handle.lib.dppo_learn_f32)
-            N.check(fn(self.handle.h, ctypes.byref(ro.as_struct()), self.flat.flat.data_ptr(),
-                       self.m.data_ptr(), self.v.data_ptr(), ctypes.byref(hp), pinned,
-                       ctypes.byref(outputs) if outputs is not None else None, stream),
-                    "dppo_learn_f32")
-            if self._cur_share is not None:  # its upload from the shared slot is now enqueued
-                self.share.used(*self._cur_share)
+            try:
+                N.check(fn(self.handle.h, ctypes.byref(ro.as_struct()),
+                           self.flat.flat.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                           ctypes.byref(hp), pinned,
+                           ctypes.byref(outputs) if outputs is not None else None, stream),
+                        "dppo_learn_f32")
+            finally:
+                # the upload from the shared slot is now enqueued (or the call failed): the slot
+                # goes from held to pending, released once the upload's event has completed
+                if self._cur_share is not None:
+                    self.share.used(*self._cur_share)
+                    self._cur_share = None
             t3 = time.perf_counter()
             hs = self.host_seconds
             hs["perms"] += t1 - t0

@@ -295,7 +295,7 @@ int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, int32_t coun
  * speculative accept scan per chunk of the word stream, an exact serial stitch, a parallel
  * assembly); identical outputs and key/pos advance.  Falls back to the serial draw (never to a
  * different result) when a stitch check fails.  opts (nullable, 3 x int64): chunks (0 = threads),
- * near-miss band W (0 = 6 sigma of the model), W multiplier x100 (0 = 600).  stats (nullable,
+ * near-miss band W (0 = 4 sigma of the model), W multiplier x100 (0 = 400).  stats (nullable,
  * 24 x int64): [0] path (0 serial, 1 parallel, 2 parallel attempt fell back), [1] chunks,
  * [2] near-miss records, [3] kept zone words, [4] replayed words, [5] max |offset|, [6] W,
  * [7] Wb, [8] scan us, [9] stitch us, [10] assembly us, [11] slowest chunk us, [12] words

@@ -134,12 +134,16 @@ def run_share(rank, world, out):
     """Global minibatches with the swap targets drawn on the host (DPPO_PERM_DEVICE=1): the same
     four learns from the same parameters and NumPy state, first with one draw per rank
     (DPPO_PERM_SHARE=0), then with the node-shared draw (drawshare.py: rank 0 draws into shared
-    memory, rank 1 uploads from it)."""
+    memory, rank 1 uploads from it).  Eight learns at T=128 and 2,048 envs per rank: a draw of
+    the 4 x 524,288 global swap targets takes milliseconds, and rank 1 sleeps before every other
+    learn, so the leader's look-ahead runs ahead of the follower's uploads (the slot-hold
+    protocol, drawshare.py, is what keeps it from drawing over one)."""
+    import time
     import torch
     import diamond
     import bench
     from gpu_helpers import SpecEnvs
-    T, Nl, D, A, n_learn = 32, 64, 4, 2, 4
+    T, Nl, D, A, n_learn = 128, 2048, 4, 2, 8
     res = {}
     init = None
     for tag, share in (("own", "0"), ("shared", "1")):
@@ -156,7 +160,9 @@ def run_share(rank, world, out):
             L.flat.flat.copy_(init)
         ro, _ = bench.synth_rollout(T, Nl, D, A, False, 0.02, 0.005, rank, agent.device)
         np.random.seed(7)
-        for _ in range(n_learn):
+        for i in range(n_learn):
+            if rank == 1 and i % 2:
+                time.sleep(0.05)
             agent.learn_device(ro)
         torch.cuda.synchronize()
         res[f"final_{tag}"] = L.flat.flat.cpu().numpy()

@@ -6,6 +6,7 @@ MT19937 key and pos); a follower whose state differs never takes one, draws itse
 holds the leader back.  The handle is a stand-in whose uploads complete at once."""
 import multiprocessing as mp
 import os
+import time
 import uuid
 
 import numpy as np
@@ -132,3 +133,83 @@ def test_a_failing_draft_does_not_stop_the_draft_worker():
         w.submit(lambda: ran.append(1), d2)
         assert d1.wait(10) and d2.wait(10) and ran == [1]
     w.stop()
+
+
+class _SlowHandle(_Handle):
+    """Uploads complete only when the test says so (``finish``)."""
+
+    def __init__(self):
+        self.done = {}
+
+    def perm_external_done(self, k):
+        return self.done.get(k, True)
+
+
+def _race_follower(name, ready, took, upload_done, q):
+    from diamond import drawshare as S
+    try:
+        ready.wait(30)
+        h = _SlowHandle()
+        share = S.NodeDrawShare(name, False, 1, 2, 64, h)
+        key = np.zeros(624, np.uint32)
+        r0 = share.follow(key, 0)      # takes draft 0 (slot 0): its learn has not run yet
+        r1 = share.follow(key, 0)      # the look-ahead follows draft 1 meanwhile
+        share.pump()                   # the next learn starts: pump() before its _targets()
+        assert r0 is not None and r1 is not None, (r0, r1)
+        took.set()
+        time.sleep(1.0)                # the leader, two learns ahead, wants slot 0 back
+        h.done[r0[0]] = False
+        share.used(r0[0], r0[1])       # the learn enqueues its upload from slot 0 ...
+        share.pump()
+        time.sleep(0.5)
+        upload_done.set()              # ... which completes only now
+        h.done[r0[0]] = True
+        deadline = time.monotonic() + 20
+        while time.monotonic() < deadline and q.empty():
+            share.pump()
+            time.sleep(0.01)
+        share.used(r1[0], r1[1])
+        share.pump()
+        q.put(("follower", 0, None))
+        share.close()
+    except Exception as e:
+        q.put(("follower", -1, repr(e)))
+
+
+@pytest.mark.timeout(120)
+def test_leader_never_reuses_a_slot_whose_follower_upload_is_not_done():
+    """A follower that took draft j holds its slot through its look-ahead's next follow() and
+    pump() until the learn's upload from the slot has completed: the leader's draft j+SLOTS
+    (same slot) must wait for that upload.  Before the fix the slot was released as soon as
+    the follower moved on to draft j+1, and the leader drew over it mid-upload."""
+    from diamond import drawshare as S
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    took, upload_done, ready = ctx.Event(), ctx.Event(), ctx.Event()
+    name = f"dppo_race_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    # the leader pre-draws drafts 0..SLOTS-1 into every slot before the follower attaches
+    pre = S.NodeDrawShare(name, True, 0, 2, 64, _Handle())
+    try:
+        for _ in range(S.SLOTS):
+            sl, gen, _ = pre.lead(np.zeros(624, np.uint32), 0, lambda kk, pp, v: pp)
+            pre.used(sl, gen)
+        pre.g[16 + 1] = 1  # the follower counts as active from the start
+        f = ctx.Process(target=_race_follower, args=(name, ready, took, upload_done, q))
+        f.start()
+        ready.set()
+        assert took.wait(60)
+        fill = lambda kk, pp, view: pp  # noqa: E731
+        sl, gen, _ = pre.lead(np.zeros(624, np.uint32), 0, fill)  # draft SLOTS -> slot 0
+        early = not upload_done.is_set()
+        pre.used(sl, gen)
+        q.put(("leader", sl, early))
+        who = {}
+        for _ in range(2):
+            tag, a, b = q.get(timeout=60)
+            who[tag] = (a, b)
+        f.join(30)
+        assert f.exitcode == 0, who
+        assert who["follower"][0] == 0, who
+        assert who["leader"] == (0, False), "leader reused slot 0 before the follower's upload"
+    finally:
+        pre.close()

@@ -110,8 +110,8 @@ def test_node_shared_draw_matches_one_draw_per_rank(tmp_path):
         assert np.array_equal(r["rng_own"], r["rng_shared"])
     assert np.array_equal(r0["final_shared"], r1["final_shared"])
     shared, own, mismatch, timeout, leader = (int(x) for x in r1["stats"])
-    assert leader == 0 and shared >= 3 and own == 0 and timeout == 0, r1["stats"]
-    assert int(r0["stats"][4]) == 1 and int(r0["stats"][0]) >= 3, r0["stats"]
+    assert leader == 0 and shared >= 7 and own == 0 and timeout == 0, r1["stats"]
+    assert int(r0["stats"][4]) == 1 and int(r0["stats"][0]) >= 7, r0["stats"]
 
 
 @pytest.mark.timeout(300)
@@ -123,11 +123,7 @@ def test_peer_exchange_drop_in_agent(tmp_path):
     assert np.array_equal(r0["trace"], r1["trace"])
 
 
-# coarse first: in one process, a coarse-grained exchange set up after an uncached exchange has run
-# learns never saw its own tagged stores (a deterministic 10 s self-test timeout on the box,
-# DESIGN.md §6 round 5) -- a process uses one memory type (DPPO_PEER_MEM is read per buffer, and
-# production sets it once), so the variants run in the order that never mixes them that way
-@pytest.mark.parametrize("variant", ["coarse", "fine", "uncached", "wrap"])
+@pytest.mark.parametrize("variant", ["uncached", "coarse", "fine", "wrap"])
 def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(monkeypatch, variant):
     """A 1-rank peer exchange in this process: every learn() then takes the multi-rank sequence
     of a node with one GPU per rank -- the advantage statistics through the exchange kernel, and
