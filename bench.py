@@ -242,6 +242,9 @@ def host_cpus():
     return aff, quota, min(aff, quota) if quota else aff
 
 
+CPU_VS_REF = "r06_cpu_baseline_vs_reference.json"
+
+
 def cpu_baselines(cfg_name):
     """One full learn() of the same workload on the host cores: the PyTorch-CPU restatement
     (oracle/ppo_torch.py: the reference's own arithmetic -- autograd, torch.distributions,
@@ -667,9 +670,28 @@ def main():
                                      "affine": gae_roofline(device, N=65536, mode=1)}
     if baseline is not None:
         tb, nb = baseline
+        # the restatement's time over the reference's own on the same learn(), measured in the
+        # build container where the reference is importable (tools/cpu_baseline_vs_reference.py;
+        # the reference never travels to this box): the factor converts the port's rate into
+        # an estimate of the reference path's rate on these cores
+        try:
+            with open(os.path.join(ROOT, "profiles", CPU_VS_REF)) as f:
+                cal = json.load(f)
+            r = float(cal.get("restatement_over_reference_time_median",
+                              cal["restatement_over_reference_time"]))
+            tb["restatement_over_reference"] = round(r, 3)
+            tb["restatement_over_reference_source"] = f"profiles/{CPU_VS_REF} ({cal['cpu']}, " \
+                                                      f"{cal['torch_threads']} threads, " \
+                                                      f"T={cal['T']} N={cal['N']})"
+            tb["reference_equivalent_value"] = round(tb["value"] * r, 1)
+        except (OSError, KeyError, ValueError):
+            pass
         out["cpu_baseline"] = tb
         out["cpu_baseline_numpy"] = nb
         out["speedup_vs_cpu_baseline"] = round(out["value"] / tb["value"], 1)
+        if "reference_equivalent_value" in tb:
+            out["speedup_vs_reference_equivalent"] = round(
+                out["value"] / tb["reference_equivalent_value"], 1)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -286,11 +286,14 @@ int device_status(const dppo_handle* h) {
   if (e == 0u) return DPPO_OK;
   const unsigned code = e & 0xffu, rank = (e >> 8) & 0xffu, idx = e >> 16;
   if (code == kErrPeerTimeout) {
+    const unsigned seen_lo = __atomic_load_n(h->err_host + 2, __ATOMIC_ACQUIRE);
+    const unsigned seen_hi = __atomic_load_n(h->err_host + 3, __ATOMIC_ACQUIRE);
     set_error("a peer exchange timed out: rank %u's word %u (slice or gradient element) did not "
-              "arrive within %.0f s (DPPO_PEER_TIMEOUT_S) -- another rank did not reach the same "
-              "all-reduce, or its publish is not visible here; that optimizer step used this "
-              "rank's gradient alone and this handle is no longer usable",
-              rank, idx, (double)h->xticks / 1e8);
+              "arrive within %.0f s (DPPO_PEER_TIMEOUT_S; exchange %u, last read 0x%08x%08x) -- "
+              "another rank did not reach the same all-reduce, or its publish is not visible "
+              "here; that optimizer step used this rank's gradient alone and this handle is no "
+              "longer usable",
+              rank, idx, (double)h->xticks / 1e8, h->xseq, seen_hi, seen_lo);
     return DPPO_ECOMM;
   }
   if (code == kErrTagTimeout) {
@@ -875,6 +878,11 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   h->sh.A = dims->act_dim;
   h->sh.continuous = dims->continuous;
   h->sh.R = D8 + 4 + (dims->continuous ? (dims->act_dim + 3) / 4 * 4 : 0);
+  // DPPO_REC_PAD=1 (A/B): pad a discrete record of 12 floats (48 B, every third one across a
+  // 128-B line) to 16 (64 B, never across one); the minibatch kernels' gathers then touch one
+  // line per record instead of 1.375 on average
+  if (const char* rp = std::getenv("DPPO_REC_PAD"))
+    if (rp[0] == '1' && !dims->continuous && h->sh.R < 16) h->sh.R = 16;
   h->mlp_ok = dims->hidden == 64 && dims->obs_dim <= 32 && dims->act_dim <= 16 &&
               mb_lds_bytes(h->sh) <= 160 * 1024 &&
               (size_t)(h->layout.total + 8) * 4 <= 160 * 1024;
@@ -950,7 +958,7 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
       set_error("hipHostMalloc (coherent error word) failed");
       rc = DPPO_EHIP;
     } else {
-      __atomic_store_n(h->err_host, 0u, __ATOMIC_RELEASE);
+      for (int k = 15; k >= 0; --k) __atomic_store_n(h->err_host + k, 0u, __ATOMIC_RELEASE);
     }
   }
   // The single-device optimizer step waits in a grid-wide fan-in: take it only when its whole

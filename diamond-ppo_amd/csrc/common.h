@@ -173,10 +173,20 @@ constexpr unsigned kErrTagTimeout = 3u;    // reduce_adam's tagged-word fan-in g
 __device__ __forceinline__ unsigned err_word(unsigned code, unsigned rank, unsigned idx) {
   return code | (rank & 0xffu) << 8 | (idx & 0xffffu) << 16;
 }
-__device__ __forceinline__ void raise_err(unsigned* err, unsigned code) {
+__device__ __forceinline__ bool raise_err(unsigned* err, unsigned code) {
   unsigned expect = 0u;  // one compare-and-swap: of two waves timing out together, the first wins
-  __hip_atomic_compare_exchange_strong(err, &expect, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_compare_exchange_strong(err, &expect, code, __ATOMIC_RELAXED,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The first cause's evidence (words 2-3 of the 64-B error block): the last value the stalled wait
+// read, written only by the wait that won raise_err.
+__device__ __forceinline__ void raise_err_seen(unsigned* err, unsigned code,
+                                               unsigned long long seen) {
+  if (raise_err(err, code)) {
+    __hip_atomic_store(err + 2, (unsigned)seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(err + 3, (unsigned)(seen >> 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 __device__ __forceinline__ bool err_set(const unsigned* err) {
   return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
@@ -380,7 +390,9 @@ __device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a, 
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
       if (late || err_set(a.err)) {
-        if (late) raise_err(a.err, err_word(kErrPeerTimeout, (unsigned)r, (unsigned)slot));
+        if (late)
+          raise_err_seen(a.err, err_word(kErrPeerTimeout, (unsigned)r, (unsigned)slot),
+                         __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
         return false;
       }
     }

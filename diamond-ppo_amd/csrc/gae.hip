@@ -375,11 +375,15 @@ __global__ __launch_bounds__(kPThreads) void gae_pipe_kernel(
           const int row = p * RP + lane / V4;
           if (row < nr) {
             const int64_t go = (int64_t)(lo + r0 + row) * N + n0 + e0;
-            xr[p] = gld<NT>((const f32x4*)(rew + go));
+            // (NT & 8: non-temporal loads of the rollout's own inputs only -- rewards and
+            // flags, staged long before -- and plain ones of the values the eval kernel has
+            // just written)
+            constexpr int NTI = (NT & 8) ? (NT | 1) : NT;
+            xr[p] = gld<NTI>((const f32x4*)(rew + go));
             xv[p] = gld<NT>((const f32x4*)(val + go));
             xn[p] = gld<NT>((const f32x4*)(nval + go));
-            xt[p] = gld<NT>((const uint32_t*)(term + go));
-            xu[p] = gld<NT>((const uint32_t*)(trunc + go));
+            xt[p] = gld<NTI>((const uint32_t*)(term + go));
+            xu[p] = gld<NTI>((const uint32_t*)(trunc + go));
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -976,6 +980,8 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
       if (a.adv_out) a.adv_out[i] = adv;
       *(f32x4*)(r + a.D8) = (f32x4){a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]),
                                     a.logp[i], adv, a.ret[i]};
+      if (!a.continuous)  // a padded record (DPPO_REC_PAD): zeros, not stale LDS
+        for (int k = a.D8 + 4; k < a.R; k += 4) *(f32x4*)(r + k) = (f32x4){0.f, 0.f, 0.f, 0.f};
       if (a.continuous) {
         const int na = a.R - a.D8 - 4;  // a multiple of 4
         const float* sa = act_s + t * a.A;
@@ -1025,6 +1031,10 @@ int launch_pipe(int nt, int grid, hipStream_t s, const float* r, const uint8_t* 
                 double* partials, int T, int N, float gamma, float c, int wt, int stagger,
                 int psleep) {
   switch (nt) {
+    case 1: return launch_pipe_nt<E, 1>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+    case 5: return launch_pipe_nt<E, 5>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+    case 8: return launch_pipe_nt<E, 8>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
+    case 12: return launch_pipe_nt<E, 12>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
     case 3: return launch_pipe_nt<E, 3>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
     case 4: return launch_pipe_nt<E, 4>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
     case 7: return launch_pipe_nt<E, 7>(grid, s, r, te, tr, v, nv, adv, ret, partials, T, N, gamma, c, wt, stagger, psleep);
@@ -1075,7 +1085,8 @@ int launch_gae(const float* r, const uint8_t* te, const uint8_t* tr, const float
     // DPPO_GAE_PSLEEP=0/1/2 overrides (A/B).
     static const int psleep =
         std::getenv("DPPO_GAE_PSLEEP") ? std::atoi(std::getenv("DPPO_GAE_PSLEEP")) : 1;
-    // DPPO_GAE_NT: the owners' streaming variant (gae_pipe_kernel NT bits; 0, 3, 4 or 7; A/B).
+    // DPPO_GAE_NT: the owners' streaming variant (gae_pipe_kernel NT bits; 0, 1, 3, 4, 5, 7, 8 or
+    // 12; A/B).
     // On cold rotating buffers (tools/gae_bench.py) non-temporal operand loads and advantage /
     // return stores (3) measured 7.25-7.59 against 7.73-7.84 us per launch at N = 8192; inside a
     // learn, where the eval kernel has just written values / next_values and the pack kernel reads

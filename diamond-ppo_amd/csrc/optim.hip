@@ -224,14 +224,17 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
       if (r < pl.world && p < n) pend |= 1u << r;
     }
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long seen = 0;  // the last word read of the lowest rank still pending
     for (unsigned k = 0;; ++k) {
 #pragma unroll
-      for (int r = 0; r < kMaxPeers; ++r) {
+      for (int r = kMaxPeers - 1; r >= 0; --r) {
         if (pend & (1u << r)) {
           const unsigned long long w = peer_get(peer_tagged(pl, r) + p);
           if ((unsigned)(w >> 32) == pl.seq) {
             x[r] = __uint_as_float((unsigned)w);
             pend &= ~(1u << r);
+          } else {
+            seen = w;
           }
         }
       }
@@ -245,7 +248,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
             const int l = __ffsll((long long)b) - 1;
             const unsigned pr = (unsigned)__shfl((int)pend, l);
             const unsigned r = (unsigned)(__ffs((int)pr) - 1);
-            if (lane == l) raise_err(err, err_word(kErrPeerTimeout, r, (unsigned)p));
+            if (lane == l) raise_err_seen(err, err_word(kErrPeerTimeout, r, (unsigned)p), seen);
           }
           return;  // parameters untouched; the handle reports the error
         }

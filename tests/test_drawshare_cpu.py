@@ -213,3 +213,62 @@ def test_leader_never_reuses_a_slot_whose_follower_upload_is_not_done():
         assert who["leader"] == (0, False), "leader reused slot 0 before the follower's upload"
     finally:
         pre.close()
+
+
+def _drop_follower(name, ready, took, q):
+    from diamond import drawshare as S
+    try:
+        ready.wait(30)
+        h = _SlowHandle()
+        share = S.NodeDrawShare(name, False, 1, 2, 64, h)
+        key = np.zeros(624, np.uint32)
+        r0 = share.follow(key, 0)      # takes draft 0 (slot 0) ...
+        share.pump()
+        assert r0 is not None and r0[0] in share.held, (r0, share.held)
+        took.set()
+        time.sleep(0.5)
+        share.drop(r0[0], r0[1])       # ... and drops it unused (a look-ahead miss)
+        assert r0[0] not in share.held
+        deadline = time.monotonic() + 20
+        while time.monotonic() < deadline and q.empty():
+            share.pump()
+            time.sleep(0.01)
+        q.put(("follower", 0, None))
+        share.close()
+    except Exception as e:
+        q.put(("follower", -1, repr(e)))
+
+
+@pytest.mark.timeout(120)
+def test_a_dropped_draft_gives_its_slot_back_without_an_upload():
+    """drop() (engine: a look-ahead miss or a failed learn) releases a held slot at once: the
+    leader's next draft into that slot proceeds although no upload from it was ever enqueued."""
+    from diamond import drawshare as S
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    took, ready = ctx.Event(), ctx.Event()
+    name = f"dppo_drop_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    pre = S.NodeDrawShare(name, True, 0, 2, 64, _Handle())
+    try:
+        for _ in range(S.SLOTS):
+            sl, gen, _ = pre.lead(np.zeros(624, np.uint32), 0, lambda kk, pp, v: pp)
+            pre.used(sl, gen)
+        pre.g[16 + 1] = 1
+        f = ctx.Process(target=_drop_follower, args=(name, ready, took, q))
+        f.start()
+        ready.set()
+        assert took.wait(60)
+        t0 = time.monotonic()
+        sl, gen, _ = pre.lead(np.zeros(624, np.uint32), 0, lambda kk, pp, v: pp)
+        waited = time.monotonic() - t0
+        pre.used(sl, gen)
+        q.put(("leader", sl, waited))
+        who = {}
+        for _ in range(2):
+            tag, a, b = q.get(timeout=60)
+            who[tag] = (a, b)
+        f.join(30)
+        assert f.exitcode == 0 and who["follower"][0] == 0, who
+        assert who["leader"][0] == 0 and 0.3 < who["leader"][1] < 15, who  # waited for drop()
+    finally:
+        pre.close()

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Round 6 diagnosis of the coarse/fine exchange-buffer failure: which
+history in one process makes a 1-rank fused exchange miss its own tagged word.  Each case runs in
+its own process as a sequence of agents (exchange-buffer memory type, golden learn trace,
+per-kernel timing on/off); every agent opens a 1-rank exchange, runs the self-test, then the
+golden learns, and is closed.  Prints one line per case: each agent's self-test result.
+
+    python tools/gpu/r06_coarse_diag.py            # every case, one subprocess each
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+U, C, F = "uncached", "coarse", "fine"
+CP, CH = "cartpole_small", "cheetah_small"
+CASES = {  # name: [(memory, golden, timing)]
+    "test order (timing)": [(U, CP, 1), (U, CH, 1), (C, CP, 1), (C, CH, 1)],
+    "test order, no timing": [(U, CP, 0), (U, CH, 0), (C, CP, 0), (C, CH, 0)],
+    "uncached cheetah > coarse": [(U, CH, 1), (C, CP, 1)],
+    "uncached cart x2 > coarse": [(U, CP, 1), (U, CP, 1), (C, CP, 1)],
+    "uncached cart,cheetah > uncached": [(U, CP, 1), (U, CH, 1), (U, CP, 1), (U, CH, 1)],
+    "coarse cart,cheetah > coarse": [(C, CP, 1), (C, CH, 1), (C, CP, 1)],
+    "uncached cart,cheetah > fine": [(U, CP, 1), (U, CH, 1), (F, CP, 1)],
+}
+
+
+def one(case):
+    sys.path[:0] = [os.path.join(ROOT, "diamond-ppo_amd"), ROOT, os.path.join(ROOT, "tests"),
+                    os.path.join(ROOT, "tests", "golden")]
+    import numpy as np
+    import torch
+    import diamond
+    from conftest import load_golden
+    from gpu_helpers import stream
+    from test_gpu_parity import experience, make_agent
+    out = []
+    for mem, name, timing in CASES[case]:
+        os.environ["DPPO_PEER_MEM"] = mem
+        z = load_golden(f"learn_{name}.npz")
+        cont = int(z["dims"][4])
+        agent = make_agent(z)
+        L = agent._learner
+        h = L.handle
+        assert not h.peer_open(1, 0, h.peer_export())
+        err = h.peer_selftest(stream())
+        info = h.peer_info()
+        out.append(f"{mem[0]}{name[:2]}:{'ok' if not err else 'FAIL ' + err[:70]}")
+        if err:
+            break
+        if timing:
+            h.set_timing(True)
+        for li in range(int(z["dims"][5])):
+            np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
+                                 int(z[f"rng_pos_before{li}"]), 0, 0.0))
+            ro = diamond.engine.stage_experience(experience(z, li), agent.device, bool(cont))
+            agent.learn_device(ro)
+        torch.cuda.synchronize()
+        out[-1] += f"(fused={info['fused']})"
+        L.close()
+    print(f"RESULT {case}: " + " | ".join(out), flush=True)
+
+
+def main():
+    if len(sys.argv) > 1:
+        return one(sys.argv[1])
+    for case in CASES:
+        r = subprocess.run([sys.executable, __file__, case], capture_output=True, text=True,
+                           timeout=150)
+        res = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+        print(res[0] if res else f"RESULT {case}: rc {r.returncode} {r.stderr[-400:]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
