@@ -248,12 +248,24 @@ unsigned next_radam_epoch(dppo_handle* h) {
   return h->radam_epoch;
 }
 
+int peer_acq();
+
 // Test-only environment hooks (a sequence number near the 32-bit wrap, a skewed self-test
 // contribution) act only with DPPO_TEST_HOOKS=1, so a stray variable cannot change a production
 // run.
 const char* test_hook(const char* name) {
   const char* e = std::getenv("DPPO_TEST_HOOKS");
   return e && e[0] == '1' ? std::getenv(name) : nullptr;
+}
+
+// DPPO_PEER_ACQ=1 (with DPPO_TEST_HOOKS=1; diagnosis of stale exchange-buffer reads): every poll
+// of a peer word behind a system-scope acquire fence
+int peer_acq() {
+  static const int v = [] {
+    const char* e = test_hook("DPPO_PEER_ACQ");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
 }
 
 template <typename T>
@@ -460,6 +472,7 @@ int peer_allreduce(dppo_handle* h, void* buf, size_t n, bool f64, hipStream_t s)
   a.seq = next_xseq(h);
   a.err = h->err_dev;
   a.timeout_ticks = h->xticks;
+  a.acq = peer_acq();
   return launch_peer_sum(a, f64, s);
 }
 
@@ -803,6 +816,7 @@ int learn_impl(dppo_handle* h, const dppo_rollout* rollout, float* params, float
           pa.seq = next_xseq(h);
           pa.err = h->err_dev;
           pa.timeout_ticks = h->xticks;
+          pa.acq = peer_acq();
         }
         // a block's intra-device fan-in starts after its peer wait: bound it like the peer wait
         const unsigned long long fan_ticks =
@@ -1751,6 +1765,7 @@ int dppo_peer_selftest(dppo_handle* h, void* stream) {
       pa.seq = next_xseq(h);
       pa.err = h->err_dev;
       pa.timeout_ticks = h->xticks;
+          pa.acq = peer_acq();
       DPPO_TRY(launch_reduce_adam(slab, 1, h->slab_stride, P, grad, h->ra_tags, 0, 0, 0.f, 0,
                                   next_radam_epoch(h), pm, pm + P, pm + 2 * P, 0.5f, -1e-3f, 1.f,
                                   0.9f, 0.999f, 1e-5f, nullptr, 1.f, 1.f, 0.f, h->err_dev,

@@ -355,6 +355,8 @@ struct PeerArgs {
   unsigned seq;           // exchange number, the same sequence on every rank (1, 2, ...)
   unsigned* err;          // the handle's sticky device error word
   unsigned long long timeout_ticks;
+  int acq;                // diagnosis (DPPO_TEST_HOOKS + DPPO_PEER_ACQ=1): a system-scope acquire
+                          // fence before every poll of a peer word
 };
 int64_t peer_buffer_bytes(int64_t cap);  // cap = elements (of up to 8 B) per parity
 int launch_peer_sum(const PeerArgs& a, bool f64, hipStream_t s);
@@ -384,8 +386,10 @@ __device__ __forceinline__ T peer_get(const T* p) {
 // a.timeout_ticks of wall clock or once the handle's error word is already set.
 __device__ __forceinline__ bool peer_wait(const unsigned* f, const PeerArgs& a, int r, int slot) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (unsigned k = 0;
-       (int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.seq) < 0; ++k) {
+  for (unsigned k = 0;; ++k) {
+    if (a.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - a.seq) >= 0)
+      break;
     __builtin_amdgcn_s_sleep(1);
     if ((k & 255u) == 255u) {
       const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;

@@ -226,6 +226,7 @@ __global__ __launch_bounds__(kRedThreads) void reduce_adam_kernel(
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     unsigned long long seen = 0;  // the last word read of the lowest rank still pending
     for (unsigned k = 0;; ++k) {
+      if (pl.acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #pragma unroll
       for (int r = kMaxPeers - 1; r >= 0; --r) {
         if (pend & (1u << r)) {

@@ -14,14 +14,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 U, C, F = "uncached", "coarse", "fine"
 CP, CH = "cartpole_small", "cheetah_small"
-CASES = {  # name: [(memory, golden, timing)]
-    "test order (timing)": [(U, CP, 1), (U, CH, 1), (C, CP, 1), (C, CH, 1)],
-    "test order, no timing": [(U, CP, 0), (U, CH, 0), (C, CP, 0), (C, CH, 0)],
-    "uncached cheetah > coarse": [(U, CH, 1), (C, CP, 1)],
-    "uncached cart x2 > coarse": [(U, CP, 1), (U, CP, 1), (C, CP, 1)],
-    "uncached cart,cheetah > uncached": [(U, CP, 1), (U, CH, 1), (U, CP, 1), (U, CH, 1)],
-    "coarse cart,cheetah > coarse": [(C, CP, 1), (C, CH, 1), (C, CP, 1)],
-    "uncached cart,cheetah > fine": [(U, CP, 1), (U, CH, 1), (F, CP, 1)],
+CASES = {  # name: [(memory, golden, timing)]; "+acq": DPPO_PEER_ACQ=1 (system-scope acquire
+    # fence before every poll of a peer word)
+    "uncached cart x2 > coarse": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
+    "uncached cart x2 > coarse +acq": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
+    "uncached cart x2 (self-test only) > coarse": [(U, CP, -1), (U, CP, -1), (C, CP, 0)],
+    "uncached cart x2 > fine": [(U, CP, 0), (U, CP, 0), (F, CP, 0)],
+    "uncached cart x2 > fine +acq": [(U, CP, 0), (U, CP, 0), (F, CP, 0)],
+    "fine cart x2 > coarse": [(F, CP, 0), (F, CP, 0), (C, CP, 0)],
+    "coarse cart x2 > fine": [(C, CP, 0), (C, CP, 0), (F, CP, 0)],
 }
 
 
@@ -34,6 +35,9 @@ def one(case):
     from conftest import load_golden
     from gpu_helpers import stream
     from test_gpu_parity import experience, make_agent
+    if case.endswith("+acq"):
+        os.environ["DPPO_TEST_HOOKS"] = "1"
+        os.environ["DPPO_PEER_ACQ"] = "1"
     out = []
     for mem, name, timing in CASES[case]:
         os.environ["DPPO_PEER_MEM"] = mem
@@ -45,12 +49,12 @@ def one(case):
         assert not h.peer_open(1, 0, h.peer_export())
         err = h.peer_selftest(stream())
         info = h.peer_info()
-        out.append(f"{mem[0]}{name[:2]}:{'ok' if not err else 'FAIL ' + err[:70]}")
+        out.append(f"{mem[0]}{name[:2]}:{'ok' if not err else 'FAIL ' + err}")
         if err:
             break
-        if timing:
+        if timing > 0:
             h.set_timing(True)
-        for li in range(int(z["dims"][5])):
+        for li in range(int(z["dims"][5]) if timing >= 0 else 0):
             np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
                                  int(z[f"rng_pos_before{li}"]), 0, 0.0))
             ro = diamond.engine.stage_experience(experience(z, li), agent.device, bool(cont))
@@ -66,9 +70,12 @@ def main():
         return one(sys.argv[1])
     for case in CASES:
         r = subprocess.run([sys.executable, __file__, case], capture_output=True, text=True,
-                           timeout=150)
+                           timeout=150, env=dict(os.environ, DPPO_PEER_DEBUG="1"))
         res = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]
+        bufs = [l.split("buffer ")[1] for l in r.stderr.splitlines()
+                if l.startswith("dppo peer: exchange buffer")]
         print(res[0] if res else f"RESULT {case}: rc {r.returncode} {r.stderr[-400:]}", flush=True)
+        print("   buffers: " + " ; ".join(bufs), flush=True)
 
 
 if __name__ == "__main__":
