@@ -892,11 +892,6 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   h->sh.A = dims->act_dim;
   h->sh.continuous = dims->continuous;
   h->sh.R = D8 + 4 + (dims->continuous ? (dims->act_dim + 3) / 4 * 4 : 0);
-  // DPPO_REC_PAD=1 (A/B): pad a discrete record of 12 floats (48 B, every third one across a
-  // 128-B line) to 16 (64 B, never across one); the minibatch kernels' gathers then touch one
-  // line per record instead of 1.375 on average
-  if (const char* rp = std::getenv("DPPO_REC_PAD"))
-    if (rp[0] == '1' && !dims->continuous && h->sh.R < 16) h->sh.R = 16;
   h->mlp_ok = dims->hidden == 64 && dims->obs_dim <= 32 && dims->act_dim <= 16 &&
               mb_lds_bytes(h->sh) <= 160 * 1024 &&
               (size_t)(h->layout.total + 8) * 4 <= 160 * 1024;
@@ -1579,6 +1574,10 @@ int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
   }
   hipIpcMemHandle_t hd;
   static_assert(sizeof(hd) == 64, "hipIpcMemHandle_t size");
+  if (test_hook("DPPO_PEER_NOIPC")) {  // (diagnosis, 1-rank exchanges only: no IPC export)
+    std::memset(out64, 0, 64);
+    return DPPO_OK;
+  }
   DPPO_HIP_CHECK(hipIpcGetMemHandle(&hd, h->xbuf));
   std::memcpy(out64, &hd, 64);
   return DPPO_OK;

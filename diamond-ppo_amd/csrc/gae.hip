@@ -980,8 +980,6 @@ __global__ __launch_bounds__(kPackTile) void pack_kernel(PackArgs a) {
       if (a.adv_out) a.adv_out[i] = adv;
       *(f32x4*)(r + a.D8) = (f32x4){a.continuous ? 0.0f : __int_as_float(((const int32_t*)a.actions)[i]),
                                     a.logp[i], adv, a.ret[i]};
-      if (!a.continuous)  // a padded record (DPPO_REC_PAD): zeros, not stale LDS
-        for (int k = a.D8 + 4; k < a.R; k += 4) *(f32x4*)(r + k) = (f32x4){0.f, 0.f, 0.f, 0.f};
       if (a.continuous) {
         const int na = a.R - a.D8 - 4;  // a multiple of 4
         const float* sa = act_s + t * a.A;

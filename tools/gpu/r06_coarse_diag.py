@@ -14,15 +14,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 U, C, F = "uncached", "coarse", "fine"
 CP, CH = "cartpole_small", "cheetah_small"
-CASES = {  # name: [(memory, golden, timing)]; "+acq": DPPO_PEER_ACQ=1 (system-scope acquire
-    # fence before every poll of a peer word)
+CASES = {  # name: [(memory, golden, mode)]; mode 0 learns, -1 self-test only, 2 kept alive (not
+    # closed); "+acq": DPPO_PEER_ACQ=1 (system-scope acquire before every poll of a peer word);
+    # "+noipc": DPPO_PEER_NOIPC=1 (the buffers are never exported with hipIpcGetMemHandle)
     "uncached cart x2 > coarse": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
-    "uncached cart x2 > coarse +acq": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
-    "uncached cart x2 (self-test only) > coarse": [(U, CP, -1), (U, CP, -1), (C, CP, 0)],
-    "uncached cart x2 > fine": [(U, CP, 0), (U, CP, 0), (F, CP, 0)],
-    "uncached cart x2 > fine +acq": [(U, CP, 0), (U, CP, 0), (F, CP, 0)],
-    "fine cart x2 > coarse": [(F, CP, 0), (F, CP, 0), (C, CP, 0)],
-    "coarse cart x2 > fine": [(C, CP, 0), (C, CP, 0), (F, CP, 0)],
+    "uncached cart x2 (kept alive) > coarse": [(U, CP, 2), (U, CP, 2), (C, CP, 0)],
+    "uncached cart x2 > coarse +noipc": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
+    "uncached cart x3 > coarse": [(U, CP, 0), (U, CP, 0), (U, CP, 0), (C, CP, 0)],
+    "uncached cart x2 > uncached > coarse": [(U, CP, 0), (U, CP, 0), (U, CP, 2), (C, CP, 0)],
+    "uncached cart x1 > coarse x2": [(U, CP, 0), (C, CP, 0), (C, CP, 0)],
+    "uncached x2 > coarse (other size: cheetah)": [(U, CP, 0), (U, CP, 0), (C, CH, 0)],
 }
 
 
@@ -38,6 +39,10 @@ def one(case):
     if case.endswith("+acq"):
         os.environ["DPPO_TEST_HOOKS"] = "1"
         os.environ["DPPO_PEER_ACQ"] = "1"
+    if case.endswith("+noipc"):
+        os.environ["DPPO_TEST_HOOKS"] = "1"
+        os.environ["DPPO_PEER_NOIPC"] = "1"
+    keep = []
     out = []
     for mem, name, timing in CASES[case]:
         os.environ["DPPO_PEER_MEM"] = mem
@@ -52,7 +57,7 @@ def one(case):
         out.append(f"{mem[0]}{name[:2]}:{'ok' if not err else 'FAIL ' + err}")
         if err:
             break
-        if timing > 0:
+        if timing == 1:
             h.set_timing(True)
         for li in range(int(z["dims"][5]) if timing >= 0 else 0):
             np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
@@ -61,7 +66,10 @@ def one(case):
             agent.learn_device(ro)
         torch.cuda.synchronize()
         out[-1] += f"(fused={info['fused']})"
-        L.close()
+        if timing == 2:
+            keep.append(agent)
+        else:
+            L.close()
     print(f"RESULT {case}: " + " | ".join(out), flush=True)
 
 
