@@ -168,6 +168,7 @@ struct dppo_handle {
   hipEvent_t loop_ready = nullptr, loop_done = nullptr;
   // peer exchange (peer.hip): this rank's exchange buffer, and every rank's as mapped here
   char* xbuf = nullptr;
+  int64_t xbytes = 0;                // its allocation size (the process pool's key)
   int64_t xcap = 0;                  // elements (of up to 8 B) per parity
   char* xpeer[kMaxPeers] = {};
   bool xmapped[kMaxPeers] = {};      // opened with hipIpcOpenMemHandle (closed on teardown)
@@ -1003,6 +1004,8 @@ int dppo_create(int device, const dppo_dims* dims, dppo_handle** out) {
   return DPPO_OK;
 }
 
+static void xpool_put(dppo_handle* h);  // (peer exchange section below)
+
 void dppo_destroy(dppo_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
@@ -1016,7 +1019,7 @@ void dppo_destroy(dppo_handle* h) {
   if (h->comm) ncclCommDestroy(h->comm);
   for (int r = 0; r < kMaxPeers; ++r)
     if (h->xmapped[r]) (void)hipIpcCloseMemHandle(h->xpeer[r]);
-  if (h->xbuf) (void)hipFree(h->xbuf);
+  xpool_put(h);  // kept for the next handle, never freed (peer_export)
   if (h->loop_out) (void)hipFree(h->loop_out);
   if (h->loop_ready) (void)hipEventDestroy(h->loop_ready);
   if (h->loop_done) (void)hipEventDestroy(h->loop_done);
@@ -1511,6 +1514,47 @@ int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id1
 }
 
 // ---- peer exchange (peer.hip) ---------------------------------------------------------------
+// Exchange buffers are never returned to the allocator: a destroyed handle's buffer goes to this
+// process-wide pool and the next handle that needs one of the same size and memory type takes it
+// (zeroed again).  Round 6: a coarse- or fine-grained exchange buffer created where
+// freed uncached ones had been (twice the same virtual address range) lost the first store to one
+// of its words for good -- a fault of address reuse below the memory model, which no fence or
+// cache-policy bit cured; with the uncached buffers kept alive the same history stayed exact.
+// Keeping every exchange buffer for the life of the process means no later allocation ever
+// reuses one's address range.  (DPPO_PEER_NOPOOL=1 with DPPO_TEST_HOOKS=1: free as before, for
+// tools/gpu/r06_coarse_diag.py.)
+struct XPoolEntry {
+  char* p;
+  int64_t bytes;
+  int mem;
+  int device;
+};
+static std::mutex g_xpool_mu;
+static std::vector<XPoolEntry> g_xpool;
+
+static void xpool_put(dppo_handle* h) {
+  if (!h->xbuf) return;
+  if (test_hook("DPPO_PEER_NOPOOL")) {
+    (void)hipFree(h->xbuf);
+  } else {
+    std::lock_guard<std::mutex> lk(g_xpool_mu);
+    g_xpool.push_back({h->xbuf, h->xbytes, h->xmem, h->device});
+  }
+  h->xbuf = nullptr;
+}
+
+static char* xpool_take(int64_t bytes, int mem, int device) {
+  std::lock_guard<std::mutex> lk(g_xpool_mu);
+  for (size_t i = 0; i < g_xpool.size(); ++i) {
+    const XPoolEntry e = g_xpool[i];
+    if (e.bytes == bytes && e.mem == mem && e.device == device) {
+      g_xpool.erase(g_xpool.begin() + (std::ptrdiff_t)i);
+      return e.p;
+    }
+  }
+  return nullptr;
+}
+
 static void peer_unmap(dppo_handle* h) {
   for (int r = 0; r < kMaxPeers; ++r) {
     if (h->xmapped[r]) (void)hipIpcCloseMemHandle(h->xpeer[r]);
@@ -1542,7 +1586,31 @@ int dppo_peer_export(dppo_handle* h, unsigned char* out64) {
     const int64_t bytes = (peer_buffer_bytes(cap) + (2 << 20) - 1) / (2 << 20) * (2 << 20);
     const char* mem = std::getenv("DPPO_PEER_MEM");
     h->xmem = !mem ? 2 : (std::strcmp(mem, "fine") == 0 ? 1 : std::strcmp(mem, "coarse") == 0 ? 0 : 2);
-    if (h->xmem == 0) {
+    // One exchange-buffer memory type per process (round 6): a coarse- or
+    // fine-grained exchange buffer created in a process that had created and freed two uncached
+    // ones lost the first store to one of its words -- the word still read its initial zero 10 s
+    // after the same lane had stored it, with or without a system-scope acquire (L1 / L2
+    // invalidate) before every read, so no scope or cache-policy bit of the publish / poll can
+    // restore it.  Every single-type history tested stayed exact; a second type is refused.
+    static std::mutex xmem_mu;
+    static int xmem_process = -1;
+    {
+      std::lock_guard<std::mutex> lk(xmem_mu);
+      // (DPPO_PEER_MIX=1 with DPPO_TEST_HOOKS=1: allowed, for tools/gpu/r06_coarse_diag.py)
+      if (xmem_process >= 0 && xmem_process != h->xmem && !test_hook("DPPO_PEER_MIX")) {
+        static const char* kName[3] = {"coarse", "fine", "uncached"};
+        set_error("dppo_peer_export: this process already created a%s %s exchange buffer; one of "
+                  "type %s in the same process is refused (DPPO_PEER_MEM must not change within a "
+                  "process: DESIGN.md section 6, round 6)",
+                  xmem_process == 2 ? "n" : "", kName[xmem_process], kName[h->xmem]);
+        return DPPO_EUNSUPPORTED;
+      }
+      xmem_process = h->xmem;
+    }
+    h->xbytes = bytes;
+    if ((h->xbuf = xpool_take(bytes, h->xmem, h->device)) != nullptr) {
+      // a pooled buffer of a destroyed handle (zeroed below)
+    } else if (h->xmem == 0) {
       DPPO_TRY(dalloc(&h->xbuf, bytes));
     } else {
       const hipError_t e = hipExtMallocWithFlags((void**)&h->xbuf, (size_t)bytes,

@@ -123,61 +123,41 @@ def test_peer_exchange_drop_in_agent(tmp_path):
     assert np.array_equal(r0["trace"], r1["trace"])
 
 
+def _one_process(variant, tmp_path):
+    from dist_scripts import fused_one_rank
+    ctx = mp.get_context("spawn")
+    out = str(tmp_path / f"fused_{variant}.txt")
+    p = ctx.Process(target=fused_one_rank.run, args=(variant, out))
+    p.start()
+    p.join(240)
+    if p.is_alive():
+        p.kill()
+    assert p.exitcode == 0, p.exitcode
+    msg = open(out).read()
+    assert msg == "ok", msg
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("variant", ["uncached", "coarse", "fine", "wrap"])
-def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(monkeypatch, variant):
-    """A 1-rank peer exchange in this process: every learn() then takes the multi-rank sequence
-    of a node with one GPU per rank -- the advantage statistics through the exchange kernel, and
-    each minibatch's gradient exchange INSIDE reduce_adam_kernel (publish the block's slice, wait
-    for every rank's flag, sum in rank order) -- and must reproduce the reference's captured
-    traces.  (Two ranks sharing this GPU take the unfused exchange: their optimizer-step grids
-    could not be resident at once; the test above.)  Variants: the exchange buffer uncached (the
-    default), coarse- or fine-grained, and the fused exchange counting on from just below the 2^32 sequence wrap (test hook)."""
-    if variant in ("coarse", "fine"):
-        monkeypatch.setenv("DPPO_PEER_MEM", variant)
-    if variant == "wrap":
-        monkeypatch.setenv("DPPO_TEST_HOOKS", "1")
-        monkeypatch.setenv("DPPO_PEER_XSEQ0", str(0xFFFFFFF0))
-    import diamond
-    from conftest import load_golden
-    from gpu_helpers import stream
-    from test_gpu_parity import experience, make_agent
-    for name in ("cartpole_small", "cheetah_small"):
-        z = load_golden(f"learn_{name}.npz")
-        T, Nn, D, A, cont, n_learn = (int(x) for x in z["dims"])
-        agent = make_agent(z)
-        L = agent._learner
-        h = L.handle
-        assert not h.peer_open(1, 0, h.peer_export())
-        assert not h.peer_selftest(stream())
-        info = h.peer_info()
-        assert info["ranks"] == 1 and info["fused"], info
-        assert info["memory"] == {"coarse": "coarse-grained", "fine": "fine-grained"}.get(
-            variant, "uncached")
-        seq0 = info["exchanges"]
-        h.set_timing(True)
-        losses, norms = [], []
-        for li in range(n_learn):
-            np.random.set_state(("MT19937", z[f"rng_state_before{li}"].astype(np.uint32),
-                                 int(z[f"rng_pos_before{li}"]), 0, 0.0))
-            ro = diamond.engine.stage_experience(experience(z, li), agent.device, bool(cont))
-            agent.learn_device(ro)
-            tr = agent.learn_trace()
-            losses += list(tr[:, 0])
-            norms += list(tr[:, 4])
-        import torch
-        torch.cuda.synchronize()
-        tm = h.timing()
-        E, M = int(z["cfg/num_epochs"]), int(z["cfg/num_minibatches"])
-        assert tm["allreduce"][1] == n_learn, tm                 # advantage statistics only
-        assert tm["reduce_adam"][1] == n_learn * E * M and tm["clip_adam"][1] == 0, tm
-        if variant == "wrap":  # the fused exchanges crossed the wrap (0 is skipped)
-            assert seq0 >= 0xFFFFFFF0 and h.peer_info()["exchanges"] < seq0, (seq0, h.peer_info())
-        np.testing.assert_allclose(losses, z["loss"], rtol=2e-5, atol=2e-5, err_msg=name)
-        np.testing.assert_allclose(norms, z["norm"], rtol=2e-5, atol=2e-5, err_msg=name)
-        for n, p in agent.network.named_parameters():
-            np.testing.assert_allclose(p.detach().cpu().numpy(), z["final/" + n], rtol=0,
-                                       atol=5e-6, err_msg=f"{name} {n}")
-        L.close()
+def test_peer_exchange_one_rank_fused_step_reproduces_reference_traces(tmp_path, variant):
+    """A 1-rank peer exchange: every learn() then takes the multi-rank sequence of a node with one
+    GPU per rank -- the advantage statistics through the exchange kernel, and each minibatch's
+    gradient exchange INSIDE reduce_adam_kernel (publish the block's slice, wait for every rank's
+    flag, sum in rank order) -- and must reproduce the reference's captured traces
+    (tests/dist_scripts/fused_one_rank.py).  (Two ranks sharing this GPU take the unfused
+    exchange: their optimizer-step grids could not be resident at once; the test above.)
+    Variants: the exchange buffer uncached (the default), coarse- or fine-grained, and the fused
+    exchange counting on from just below the 2^32 sequence wrap (test hook).  Each variant runs in
+    a process of its own: the memory type is one per process (DESIGN.md §6 round 6 -- a coarse- or
+    fine-grained buffer created after two uncached ones in one process lost a store)."""
+    _one_process(variant, tmp_path)
+
+
+@pytest.mark.timeout(300)
+def test_peer_exchange_refuses_a_second_memory_type_in_one_process(tmp_path):
+    """dppo_peer_export refuses an exchange buffer whose memory type differs from the one this
+    process already created (the allocation history that lost a store)."""
+    _one_process("mixed", tmp_path)
 
 
 def _bench_line(cmd, timeout=280):

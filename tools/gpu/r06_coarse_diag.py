@@ -16,14 +16,16 @@ U, C, F = "uncached", "coarse", "fine"
 CP, CH = "cartpole_small", "cheetah_small"
 CASES = {  # name: [(memory, golden, mode)]; mode 0 learns, -1 self-test only, 2 kept alive (not
     # closed); "+acq": DPPO_PEER_ACQ=1 (system-scope acquire before every poll of a peer word);
-    # "+noipc": DPPO_PEER_NOIPC=1 (the buffers are never exported with hipIpcGetMemHandle)
+    # "+noipc": DPPO_PEER_NOIPC=1 (the buffers are never exported with hipIpcGetMemHandle);
+    # "+nopool": DPPO_PEER_NOPOOL=1 (exchange buffers freed at handle destruction, the round-5
+    # behaviour; since round 6 they stay in a process pool and are never freed)
+    "uncached cart x2 > coarse +nopool": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
+    "uncached cart x2 > fine +nopool": [(U, CP, 0), (U, CP, 0), (F, CP, 0)],
     "uncached cart x2 > coarse": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
-    "uncached cart x2 (kept alive) > coarse": [(U, CP, 2), (U, CP, 2), (C, CP, 0)],
-    "uncached cart x2 > coarse +noipc": [(U, CP, 0), (U, CP, 0), (C, CP, 0)],
+    "uncached cart x2 > fine": [(U, CP, 0), (U, CP, 0), (F, CP, 0)],
     "uncached cart x3 > coarse": [(U, CP, 0), (U, CP, 0), (U, CP, 0), (C, CP, 0)],
-    "uncached cart x2 > uncached > coarse": [(U, CP, 0), (U, CP, 0), (U, CP, 2), (C, CP, 0)],
-    "uncached cart x1 > coarse x2": [(U, CP, 0), (C, CP, 0), (C, CP, 0)],
-    "uncached x2 > coarse (other size: cheetah)": [(U, CP, 0), (U, CP, 0), (C, CH, 0)],
+    "test order (timing)": [(U, CP, 1), (U, CH, 1), (C, CP, 1), (C, CH, 1), (F, CP, 1),
+                            (F, CH, 1)],
 }
 
 
@@ -36,9 +38,13 @@ def one(case):
     from conftest import load_golden
     from gpu_helpers import stream
     from test_gpu_parity import experience, make_agent
+    os.environ["DPPO_TEST_HOOKS"] = "1"  # mixed memory types are refused since round 6 ...
+    os.environ["DPPO_PEER_MIX"] = "1"    # ... except under this diagnosis hook
     if case.endswith("+acq"):
         os.environ["DPPO_TEST_HOOKS"] = "1"
         os.environ["DPPO_PEER_ACQ"] = "1"
+    if case.endswith("+nopool"):
+        os.environ["DPPO_PEER_NOPOOL"] = "1"
     if case.endswith("+noipc"):
         os.environ["DPPO_TEST_HOOKS"] = "1"
         os.environ["DPPO_PEER_NOIPC"] = "1"
