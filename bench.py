@@ -428,6 +428,9 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "instrumented_ms_per_step": (round(elapsed_instr / steps * 1e3, 4)
                                      if elapsed_instr else None),
         "host_ms_per_step": host,
+        # where the host's permutation draws ran (csrc/perm.cpp: the least busy L3 domain at first
+        # use, re-chosen when draws turn slow -- engine._watch_draw)
+        "host_placement": dict(NN.perm_domain(), repin_requests=agent._learner.repin_requests),
         # the host's own work per learn (draws on the draft thread + the launching thread's
         # calls), excluding time spent blocked on the device
         "host_work_ms_per_step": round(host["draw"] + host["enqueue"] + host["draft_start"]

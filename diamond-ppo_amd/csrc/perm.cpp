@@ -333,6 +333,55 @@ int main_thread_cpu() {
   return *p ? std::atoi(p) : -1;
 }
 
+// Busy fraction of every CPU over a short window, from two reads of /proc/stat (host-wide counters:
+// on a shared box they include the other tenants' load).  busy[c] < 0 where unknown.
+bool cpu_busy(std::vector<double>* busy, int window_ms) {
+  auto read = [](std::vector<std::pair<unsigned long long, unsigned long long>>* v) {
+    FILE* f = std::fopen("/proc/stat", "r");
+    if (!f) return false;
+    char line[512];
+    v->assign(CPU_SETSIZE, {0ull, 0ull});
+    while (std::fgets(line, sizeof(line), f)) {
+      int cpu = -1;
+      unsigned long long x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (std::sscanf(line, "cpu%d %llu %llu %llu %llu %llu %llu %llu %llu", &cpu, x, x + 1,
+                      x + 2, x + 3, x + 4, x + 5, x + 6, x + 7) >= 5 &&
+          cpu >= 0 && cpu < CPU_SETSIZE) {
+        unsigned long long tot = 0;
+        for (unsigned long long y : x) tot += y;
+        (*v)[cpu] = {tot, x[3] + x[4]};  // (total, idle + iowait)
+      }
+    }
+    std::fclose(f);
+    return true;
+  };
+  std::vector<std::pair<unsigned long long, unsigned long long>> a, b;
+  if (!read(&a)) return false;
+  std::this_thread::sleep_for(std::chrono::milliseconds(window_ms));
+  if (!read(&b)) return false;
+  busy->assign(CPU_SETSIZE, -1.0);
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    const unsigned long long dt = b[c].first - a[c].first, di = b[c].second - a[c].second;
+    if (b[c].first > a[c].first) (*busy)[c] = 1.0 - (double)di / (double)dt;
+  }
+  return true;
+}
+
+double domain_busy(const cpu_set_t& d, const std::vector<double>& busy) {
+  double s = 0.0;
+  int n = 0;
+  for (int c = 0; c < CPU_SETSIZE && c < (int)busy.size(); ++c)
+    if (CPU_ISSET(c, &d) && busy[c] >= 0.0) {
+      s += busy[c];
+      ++n;
+    }
+  return n ? s / n : 0.0;
+}
+
+std::atomic<int> g_dom_first{-1};       // first CPU of the swap pool's L3 domain
+std::atomic<int> g_dom_busy_pct{-1};    // its busy fraction when chosen (%)
+std::atomic<int> g_repins{0};
+
 // Where the swap workers (and the drawing thread) run.  The swap chain of an epoch reads the
 // targets the drawing thread just wrote, so they share one L3 (EPYC 9575F, 4 x 524,288: 1.3 ms
 // in one L3 against 3-4 ms placed freely and 2.25 ms on one thread).  And that L3 is not the
@@ -364,17 +413,54 @@ bool l3_domain(int mode, cpu_set_t* out) {
     doms.push_back(d);
   }
   if (!doms.empty()) {
+    // Least-loaded domains first (round 6: on the shared GPU box a draw pinned to a CCD that other
+    // tenants kept busy ran 6x slower -- 13.2 ms per learn instead of 2.2, the whole C3 learn
+    // host-bound at 75 M env-steps/s instead of 286 M); DPPO_PERM_BY_LOAD=0 keeps CPU order.
+    static const bool by_load = [] {
+      const char* e = std::getenv("DPPO_PERM_BY_LOAD");
+      return !(e && e[0] == '0');
+    }();
+    std::vector<double> busy;
+    std::vector<double> load(doms.size(), 0.0);
+    if (by_load && doms.size() > 1 && cpu_busy(&busy, 25)) {
+      for (size_t i = 0; i < doms.size(); ++i) load[i] = domain_busy(doms[i], busy);
+      std::vector<size_t> order(doms.size());
+      for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+      std::stable_sort(order.begin(), order.end(),
+                       [&](size_t x, size_t y) { return load[x] < load[y]; });
+      std::vector<cpu_set_t> sorted;
+      std::vector<double> sl;
+      for (size_t i : order) {
+        sorted.push_back(doms[i]);
+        sl.push_back(load[i]);
+      }
+      doms.swap(sorted);
+      load.swap(sl);
+    }
     // one process per GPU (torchrun's LOCAL_RANK): spread the ranks' pools over the domains
     // instead of stacking every rank's draft and swap threads on the first one
     const char* lr = std::getenv("LOCAL_RANK");
     const size_t k = lr ? (size_t)std::max(0, std::atoi(lr)) % doms.size() : 0;
     *out = doms[k];
+    for (int c = 0; c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, out)) {
+        g_dom_first.store(c);
+        break;
+      }
+    g_dom_busy_pct.store((int)(100.0 * load[k] + 0.5));
     return true;
   }
   // every allowed CPU shares the main thread's L3 (a cpuset of one CCD): the caller's L3 still
   // beats an unpinned pool or one thread (measured equal to mode 2 once the slot waits moved off
   // the draft thread)
-  return home >= 0 && l3_of(home, allowed, out) && CPU_ISSET(home, out);
+  const bool ok = home >= 0 && l3_of(home, allowed, out) && CPU_ISSET(home, out);
+  if (ok)
+    for (int c = 0; c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, out)) {
+        g_dom_first.store(c);
+        break;
+      }
+  return ok;
 }
 
 // Persistent swap workers: epoch c's swap chain runs while epoch c+1 is drawn, without a thread
@@ -425,6 +511,7 @@ class SwapPool {
     spin_ms_ = sp ? std::atoi(sp) : 0;
     const char* pe = std::getenv("DPPO_PERM_PIN");
     const int mode = pe ? std::atoi(pe) : 2;
+    mode_ = mode;
     pinned_ = mode != 0 && l3_domain(mode, &l3_);
     for (int i = 0; i < nw; ++i) {
       std::thread t([this] { run(); });
@@ -437,13 +524,37 @@ class SwapPool {
   // A draft thread (not the main thread: its affinity would be inherited by every thread it
   // starts later) joins the workers' L3 domain, once.
   bool pinned() const { return pinned_; }
-  const cpu_set_t* cpus() const { return pinned_ ? &l3_ : nullptr; }
+  // the pool's domain (a copy: repin() may replace it)
+  bool cpus(cpu_set_t* out) {
+    if (!pinned_) return false;
+    std::lock_guard<std::mutex> g(dom_mu_);
+    *out = l3_;
+    return true;
+  }
   void pin_caller() {
-    static thread_local bool done = false;
-    if (done || !pinned_) return;
-    done = true;
-    if ((pid_t)syscall(SYS_gettid) != getpid())
-      pthread_setaffinity_np(pthread_self(), sizeof(l3_), &l3_);
+    static thread_local unsigned done = 0;  // the domain generation this thread is pinned to
+    if (!pinned_) return;
+    const unsigned gen = gen_.load(std::memory_order_acquire);
+    if (done == gen + 1) return;
+    done = gen + 1;
+    if ((pid_t)syscall(SYS_gettid) != getpid()) {
+      cpu_set_t d;
+      cpus(&d);
+      pthread_setaffinity_np(pthread_self(), sizeof(d), &d);
+    }
+  }
+  // Choose the domain again by load (another tenant may have taken ours): the workers and the
+  // pinned callers move at their next job.  Returns whether the domain changed.
+  bool repin() {
+    if (!pinned_ || mode_ != 2) return false;
+    cpu_set_t d;
+    if (!l3_domain(2, &d)) return false;
+    std::lock_guard<std::mutex> g(dom_mu_);
+    if (CPU_EQUAL(&d, &l3_)) return false;
+    l3_ = d;
+    gen_.fetch_add(1, std::memory_order_acq_rel);
+    g_repins.fetch_add(1, std::memory_order_relaxed);
+    return true;
   }
 
  private:
@@ -465,6 +576,7 @@ class SwapPool {
         q_.pop_front();
         nq_.fetch_sub(1, std::memory_order_relaxed);
       }
+      pin_caller();  // (a worker follows repin() at its next job)
       apply_swaps(job.a, job.j, job.n);
       std::lock_guard<std::mutex> g(job.b->mu);
       if (--job.b->left == 0) job.b->cv.notify_all();
@@ -475,7 +587,10 @@ class SwapPool {
   std::deque<Job> q_;
   std::atomic<int> nq_{0};
   int spin_ms_ = 0;
+  int mode_ = 0;
   bool pinned_ = false;
+  std::mutex dom_mu_;
+  std::atomic<unsigned> gen_{0};
   cpu_set_t l3_;
 };
 
@@ -520,7 +635,8 @@ extern "C" int dppo_perm_targets_numpy(uint32_t* key, int32_t* pos, int64_t n, i
     return e ? std::atoi(e) : 0;
   }();
   if (ring_mode && n * count >= (1 << 20)) {
-    RingBlocks ring(g.mt, SwapPool::get().cpus());
+    cpu_set_t dom;
+    RingBlocks ring(g.mt, SwapPool::get().cpus(&dom) ? &dom : nullptr);
     int p = g.pos;
     const uint32_t* blk = draw_targets_from(ring, g.out, p, n, count, out);
     if (blk != g.out) {
@@ -603,8 +719,9 @@ int perm_start(uint32_t* key, int32_t* pos, int64_t n, int32_t count, int32_t* o
     return e ? std::atoi(e) : 1;
   }();
   std::unique_ptr<RingBlocks> ring;
+  cpu_set_t dom;
   if (t->pooled && ring_mode && n * count >= (1 << 20))
-    ring.reset(new RingBlocks(g.mt, SwapPool::get().cpus()));
+    ring.reset(new RingBlocks(g.mt, SwapPool::get().cpus(&dom) ? &dom : nullptr));
   g_calls.fetch_add(1, std::memory_order_relaxed);
   if (t->pooled) g_pooled.fetch_add(1, std::memory_order_relaxed);
   if (ring) g_ringed.fetch_add(1, std::memory_order_relaxed);
@@ -652,6 +769,26 @@ extern "C" int dppo_perm_numpy_async(uint32_t* key, int32_t* pos, int64_t n, int
   const int rc = perm_start(key, pos, n, count, out, t);
   *ticket = t;
   return rc;
+}
+
+extern "C" int dppo_perm_repin(int64_t* out4) {
+  const bool moved = SwapPool::get().repin();
+  if (out4) {
+    out4[0] = moved ? 1 : 0;
+    out4[1] = g_dom_first.load();
+    out4[2] = g_dom_busy_pct.load();
+    out4[3] = g_repins.load();
+  }
+  return DPPO_OK;
+}
+
+extern "C" int dppo_perm_domain(int64_t* out3) {
+  if (!out3) return DPPO_EINVAL;
+  (void)SwapPool::get();
+  out3[0] = g_dom_first.load();
+  out3[1] = g_dom_busy_pct.load();
+  out3[2] = g_repins.load();
+  return DPPO_OK;
 }
 
 extern "C" int dppo_perm_stats(int64_t* out3) {

@@ -32,7 +32,7 @@ EXPORTED = [
     "dppo_learn_f32", "dppo_minibatch_grad_f32", "dppo_prepare_f32", "dppo_clip_adam_f32",
     "dppo_perm_buffer", "dppo_perm_external", "dppo_perm_external_done", "dppo_get_trace", "dppo_perm_numpy", "dppo_comm_unique_id",
     "dppo_comm_init", "dppo_set_timing", "dppo_get_timing", "dppo_learn_targets_f32",
-    "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_resolve", "dppo_perm_resolve_scratch", "dppo_perm_resolve_ex", "dppo_global_minibatch_lists", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
+    "dppo_perm_targets_numpy", "dppo_perm_targets_numpy_par", "dppo_perm_par_stats", "dppo_perm_numpy_async", "dppo_perm_wait", "dppo_perm_stats", "dppo_perm_repin", "dppo_perm_domain", "dppo_perm_resolve", "dppo_perm_resolve_scratch", "dppo_perm_resolve_ex", "dppo_global_minibatch_lists", "dppo_act_f32", "dppo_act_squash_f32", "dppo_loopback_group",
     "dppo_status", "dppo_fanin_selftest", "dppo_actor_forward_f32",
     "dppo_peer_export", "dppo_peer_open", "dppo_peer_close", "dppo_peer_allreduce", "dppo_peer_info",
     "dppo_peer_selftest",
@@ -139,6 +139,8 @@ def load():
         "dppo_perm_targets_numpy": (ctypes.c_int, [vp, P(i32), i64, i32, vp]),
         "dppo_perm_targets_numpy_par": (ctypes.c_int, [vp, P(i32), i64, i32, vp, i32, vp, vp]),
         "dppo_perm_par_stats": (ctypes.c_int, [P(i64)]),
+        "dppo_perm_repin": (ctypes.c_int, [vp]),
+        "dppo_perm_domain": (ctypes.c_int, [P(i64)]),
         "dppo_perm_numpy_async": (ctypes.c_int, [vp, P(i32), i64, i32, vp, P(vp)]),
         "dppo_perm_wait": (ctypes.c_int, [vp]),
         "dppo_perm_stats": (ctypes.c_int, [P(i64)]),
@@ -272,6 +274,20 @@ def perm_targets_numpy_par(key: np.ndarray, pos: int, n: int, count: int, out: n
                                              out.ctypes.data, int(threads), opts.ctypes.data,
                                              st.ctypes.data), "dppo_perm_targets_numpy_par")
     return int(p.value), {k: int(st[i]) for i, k in enumerate(PAR_STATS)}
+
+
+def perm_repin() -> dict:
+    """Choose the permutation pool's L3 domain again by load (csrc/perm.cpp; blocks ~25 ms)."""
+    out = (ctypes.c_int64 * 4)()
+    check(load().dppo_perm_repin(out), "dppo_perm_repin")
+    return {"moved": bool(out[0]), "first_cpu": out[1], "busy_pct": out[2], "repins": out[3]}
+
+
+def perm_domain() -> dict:
+    """{first_cpu, busy_pct, repins} of the permutation pool's L3 domain (-1: not pinned)."""
+    out = (ctypes.c_int64 * 3)()
+    check(load().dppo_perm_domain(out), "dppo_perm_domain")
+    return {"first_cpu": out[0], "busy_pct": out[1], "repins": out[2]}
 
 
 def perm_par_stats() -> dict:

@@ -285,6 +285,16 @@ int dppo_perm_wait(void* ticket);
  * DPPO_PERM_PIN=3 pins the pool to every allowed CPU (no cache-topology lookup). */
 int dppo_perm_stats(int64_t* out3);
 
+/* Host placement of the permutation draws (host only; no reference counterpart -- the reference
+ * draws on its own Python thread, diamond/ppo.py:254).  The swap pool and the drawing thread run
+ * in one L3 domain, chosen at first use as the least busy one by a /proc/stat sample
+ * (DPPO_PERM_BY_LOAD=0: CPU order).  dppo_perm_repin chooses again (a ~25 ms sample; call it off
+ * the launching thread) and moves the pool at its next job: out4 (nullable) = {moved, first CPU of
+ * the domain, its busy % when chosen, re-pins so far}.  dppo_perm_domain reports the last three
+ * without sampling. */
+int dppo_perm_repin(int64_t* out4);
+int dppo_perm_domain(int64_t* out3);
+
 /* The MT19937 half of dppo_perm_numpy: the Fisher-Yates swap targets out[c][i] = j_i
  * (i = n-1 .. 1; out[c][0] = 0) of `count` successive permutations, advancing key/pos exactly
  * as dppo_perm_numpy does.  Host only.  Draws of >= 2^22 targets run the parallel form below on

@@ -505,3 +505,77 @@ def test_perm_resolve_scratch_contract():
     big = N.perm_resolve_scratch(8388608, 4)
     assert 4 * 4 * 8388608 < big < 5 * 4 * 8388608
     assert N.perm_resolve_scratch(-1, 4) == -1 and N.perm_resolve_scratch(8, -1) == -1
+
+
+def test_slow_draws_request_one_repin_off_the_launching_thread(monkeypatch):
+    """engine._watch_draw: two draws in a row above 2.5x the recent median (and 4 ms) queue one
+    re-choice of the swap pool's L3 domain on the draft worker -- never on the calling thread,
+    and not again within REPIN_EVERY_S."""
+    import threading
+    from diamond import engine as E
+    calls = []
+
+    class Worker:
+        def submit(self, fn, done):
+            calls.append((fn, threading.current_thread().name))
+
+    L = object.__new__(E.NativeLearner)
+    L._draw_hist = __import__("collections").deque(maxlen=8)
+    L._slow_draws, L._last_repin, L.repin_requests = 0, 0.0, 0
+    L.device_shuffle, L._worker = False, Worker()
+    L.cfg, L.perm_n = type("C", (), {"num_epochs": 4})(), 1 << 20
+    for t in [0.002] * 6:
+        L._watch_draw(t)
+    L._watch_draw(0.013)
+    assert not calls                      # one slow draw: no action
+    L._watch_draw(0.013)
+    assert len(calls) == 1 and calls[0][0] is E.N.perm_repin and L.repin_requests == 1
+    L._watch_draw(0.013)
+    L._watch_draw(0.013)
+    assert len(calls) == 1                # rate-limited
+    L.device_shuffle = True               # targets-only draws do not use the pool
+    L._last_repin = 0.0
+    for t in [0.02, 0.02, 0.02]:
+        L._watch_draw(t)
+    assert len(calls) == 1
+
+
+def test_a_domain_busy_from_the_first_learn_is_left_too():
+    """Before the draw history has a median, a draw above ~4x the healthy rate counts as slow."""
+    from diamond import engine as E
+    calls = []
+
+    class Worker:
+        def submit(self, fn, done):
+            calls.append(fn)
+
+    L = object.__new__(E.NativeLearner)
+    L._draw_hist = __import__("collections").deque(maxlen=8)
+    L._slow_draws, L._last_repin, L.repin_requests = 0, 0.0, 0
+    L.device_shuffle, L._worker = False, Worker()
+    L.cfg, L.perm_n = type("C", (), {"num_epochs": 4})(), 1 << 20   # C3: 4 x 1,048,576 entries
+    L._watch_draw(0.0132)
+    L._watch_draw(0.0131)
+    assert len(calls) == 1 and L.repin_requests == 1
+
+
+def test_perm_pool_domain_and_repin_keep_draws_numpy_exact():
+    """The pool's placement calls report and re-choose without changing any draw."""
+    import numpy as np
+    from diamond import _native as N
+    n = 1 << 16
+    key, pos, _ = N.mt_state(np.random.RandomState(3))
+    a = np.empty(4 * n, np.int32)
+    b = np.empty(4 * n, np.int32)
+    k1 = key.copy()
+    p1 = N.perm_numpy(k1, pos, n, 4, a)
+    d = N.perm_domain()
+    assert set(d) == {"first_cpu", "busy_pct", "repins"}
+    r = N.perm_repin()
+    assert set(r) == {"moved", "first_cpu", "busy_pct", "repins"}
+    k2 = key.copy()
+    p2 = N.perm_numpy(k2, pos, n, 4, b)
+    rs = np.random.RandomState(3)
+    ref = np.concatenate([rs.permutation(n) for _ in range(4)])
+    assert np.array_equal(a, ref) and np.array_equal(b, ref) and p1 == p2
+    assert np.array_equal(k1, k2)
