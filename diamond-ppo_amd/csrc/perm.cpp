@@ -413,12 +413,20 @@ bool l3_domain(int mode, cpu_set_t* out) {
     doms.push_back(d);
   }
   if (!doms.empty()) {
-    // Least-loaded domains first (round 6: on the shared GPU box a draw pinned to a CCD that other
-    // tenants kept busy ran 6x slower -- 13.2 ms per learn instead of 2.2, the whole C3 learn
-    // host-bound at 75 M env-steps/s instead of 286 M); DPPO_PERM_BY_LOAD=0 keeps CPU order.
+    // Busy domains last (round 6: on the shared GPU box a draw pinned to a CCD that other tenants
+    // kept busy ran 6x slower -- 13.2 ms per learn instead of 2.2, the whole C3 learn host-bound
+    // at 75 M env-steps/s instead of 286 M).  CPU order stays the preference among the domains
+    // under DPPO_PERM_BUSY_MAX (default 30 %) busy: a first version that sorted every domain by
+    // load moved the pool off its usual CCD over fractions of a percent and the same learn lost
+    // 0.7 ms to slower swaps there (memory placement), so only a busy domain is passed over; the
+    // busy ones follow, least busy first.  DPPO_PERM_BY_LOAD=0: CPU order only.
     static const bool by_load = [] {
       const char* e = std::getenv("DPPO_PERM_BY_LOAD");
       return !(e && e[0] == '0');
+    }();
+    static const double busy_max = [] {
+      const char* e = std::getenv("DPPO_PERM_BUSY_MAX");
+      return e ? std::atof(e) / 100.0 : 0.30;
     }();
     std::vector<double> busy;
     std::vector<double> load(doms.size(), 0.0);
@@ -426,8 +434,11 @@ bool l3_domain(int mode, cpu_set_t* out) {
       for (size_t i = 0; i < doms.size(); ++i) load[i] = domain_busy(doms[i], busy);
       std::vector<size_t> order(doms.size());
       for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-      std::stable_sort(order.begin(), order.end(),
-                       [&](size_t x, size_t y) { return load[x] < load[y]; });
+      std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+        const bool bx = load[x] >= busy_max, by = load[y] >= busy_max;
+        if (bx != by) return by;          // idle enough first, in CPU order
+        return bx && load[x] < load[y];   // then the busy ones, least busy first
+      });
       std::vector<cpu_set_t> sorted;
       std::vector<double> sl;
       for (size_t i : order) {
