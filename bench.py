@@ -48,7 +48,8 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "diamond-ppo_amd"))
+# DPPO_PY_ROOT (A/B timing only): import the diamond package from another tree
+sys.path.insert(0, os.environ.get("DPPO_PY_ROOT") or os.path.join(ROOT, "diamond-ppo_amd"))
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy 6290
 FP32_PEAK_TFLOPS = 157.3    # MI355X fp32 MFMA (= vector) dense peak
@@ -430,7 +431,8 @@ def run_config(name, world, rank, dist, device, steps, warmup, kernel_timing=Tru
         "host_ms_per_step": host,
         # where the host's permutation draws ran (csrc/perm.cpp: the least busy L3 domain at first
         # use, re-chosen when draws turn slow -- engine._watch_draw)
-        "host_placement": dict(NN.perm_domain(), repin_requests=agent._learner.repin_requests),
+        "host_placement": dict(getattr(NN, "perm_domain", dict)(),  # (absent: an A/B tree)
+                               repin_requests=getattr(agent._learner, "repin_requests", None)),
         # the host's own work per learn (draws on the draft thread + the launching thread's
         # calls), excluding time spent blocked on the device
         "host_work_ms_per_step": round(host["draw"] + host["enqueue"] + host["draft_start"]

@@ -391,11 +391,6 @@ class NativeLearner:
         # call).  Draft thread: "draw" (the permutation draws: the host's own work per learn).
         self.host_seconds = {"perms": 0.0, "enqueue": 0.0, "draft_start": 0.0, "draw": 0.0,
                              "slot_wait": 0.0, "calls": 0, "lookahead_hits": 0}
-        # host-load guard (round 6): draws that turn slow re-choose the swap pool's L3 domain
-        self._draw_hist = collections.deque(maxlen=8)
-        self._slow_draws = 0
-        self._last_repin = 0.0
-        self.repin_requests = 0
         self.lookahead = os.environ.get("DPPO_PERM_LOOKAHEAD", "1") != "0"
         # Where the Fisher-Yates swaps run.  The host's swap chain is cache-miss bound once the
         # [E][B] permutations outgrow the caches (C5 on one GPU, E*B = 33.5 M: ~46 ms of host
@@ -406,15 +401,11 @@ class NativeLearner:
         self.device_shuffle = (env == "1") if env in ("0", "1") else (
             cfg.num_epochs * self.perm_n >= self.PERM_DEVICE_MIN)
         # look-ahead drafts in flight (FIFO), each chained on its predecessor's final RNG state;
-        # DPPO_PERM_DEPTH (default 3) of them, in the handle's 4 pinned slots beside the one the
-        # current learn uploads from -- a slow draw (host jitter) is absorbed instead of stalling
-        # the next learn.  (Two deep through round 5: a draft could only start once the slot
-        # whose upload was three learns back had landed, so on a loaded host -- draws 2-2.7 ms
-        # against a 3.6 ms device learn -- the draft thread idled between drafts and the C3
-        # learn went host-bound at ~230 M env-steps/s.)
+        # DPPO_PERM_DEPTH (default 2) of them, in the handle's 3 pinned slots beside the one the
+        # current learn uploads from -- two deep, a slow draw (host jitter) is absorbed instead
+        # of stalling the next learn
         self._drafts = collections.deque()
-        self.draft_depth = max(1, min(N.PERM_SLOTS - 1,
-                                      int(os.environ.get("DPPO_PERM_DEPTH", "3"))))
+        self.draft_depth = max(1, min(2, int(os.environ.get("DPPO_PERM_DEPTH", "2"))))
         self._slot = 0
         self._worker = None
         self._closed = False
@@ -706,7 +697,6 @@ class NativeLearner:
             self._finish(d)
             if d["ok"]:
                 self.host_seconds["draw"] += d["t_draw"]
-                self._watch_draw(d["t_draw"])
             if (d["ok"] and d["device"] == self.device_shuffle and d["pos_in"] == pos
                     and np.array_equal(d["key_in"], key)):
                 self._slot = d["slot"]
@@ -725,35 +715,6 @@ class NativeLearner:
         self.host_seconds["draw"] += time.perf_counter() - t0
         N.set_mt_state(st, key, pos)
         return buf, key, pos
-
-    # A draw is "slow" at > REPIN_FACTOR x the median of the last 8 and > REPIN_FLOOR_S.
-    REPIN_FACTOR, REPIN_FLOOR_S, REPIN_EVERY_S = 2.5, 0.004, 5.0
-
-    def _watch_draw(self, t: float):
-        """Host-load guard.  The full-permutation draws (below PERM_DEVICE_MIN) run on the draft
-        thread and the swap pool, pinned to one L3 domain (csrc/perm.cpp); on a shared host another
-        tenant can saturate that domain -- one bench run on the box drew 6x slower for the whole
-        run (13.2 ms per C3 learn instead of 2.2: host-bound at 75 M env-steps/s).  Two slow draws
-        in a row queue a re-choice of the domain by load on the draft thread (the /proc/stat sample
-        takes ~25 ms there, never on the launching thread), at most every REPIN_EVERY_S."""
-        hist = self._draw_hist
-        # (against the recent median; before there is one, against ~4x the measured healthy rate
-        # of ~0.5 ns per drawn entry, so a domain that is busy from the first learn is left too).
-        # The median of <= 8 floats in plain Python: the first np.median call of a process costs
-        # 4-18 ms of lazy numpy set-up, and it fell on the first timed learn of bench.py -- one
-        # stall that took C3's 20-learn line from 286 to 230 M env-steps/s (round 6 A/B)
-        ref = (sorted(hist)[len(hist) // 2] * self.REPIN_FACTOR if len(hist) >= 4
-               else 2e-9 * self.cfg.num_epochs * self.perm_n)
-        slow = t > self.REPIN_FLOOR_S and t > ref
-        hist.append(t)
-        self._slow_draws = self._slow_draws + 1 if slow else 0
-        now = time.monotonic()
-        if (self._slow_draws >= 2 and not self.device_shuffle and self._worker is not None
-                and now - self._last_repin > self.REPIN_EVERY_S):
-            self._slow_draws = 0
-            self._last_repin = now
-            self.repin_requests += 1
-            self._worker.submit(N.perm_repin, threading.Event())
 
     def learn(self, ro: DeviceRollout, lr: float, outputs: N.LearnOutputs | None = None):
         cfg = self.cfg
