@@ -136,7 +136,7 @@ struct dppo_handle {
   hipEvent_t perms_free[2] = {nullptr, nullptr};  // the last learn reading device slot k is done
   bool perms_free_valid[2] = {false, false};
   // two pinned host staging slots, each with the event that marks its upload done
-  // kPermSlots pinned host staging slots: one being uploaded, the rest ready or being drawn
+  // kPermSlots pinned host staging slots: one being uploaded, one ready, one being drawn
   int32_t* perms_pinned[kPermSlots] = {};
   hipEvent_t perm_copy_done[kPermSlots] = {};
   bool perm_copy_pending[kPermSlots] = {};

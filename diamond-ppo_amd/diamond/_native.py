@@ -22,7 +22,7 @@ DPPO_ECOMM = -5
 MAX_TENSORS = 16
 GAE_EXACT, GAE_AFFINE = 0, 1  # dppo_set_gae_mode
 TRACE_FIELDS = 5
-PERM_SLOTS = 4  # pinned permutation staging slots per handle (include/dppo.h DPPO_PERM_SLOTS)
+PERM_SLOTS = 3  # pinned permutation staging slots per handle (include/dppo.h DPPO_PERM_SLOTS)
 PERM_EXT_SLOTS = 8  # external (caller-owned) staging slots per handle (DPPO_PERM_EXT_SLOTS)
 
 EXPORTED = [

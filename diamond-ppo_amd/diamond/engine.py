@@ -406,15 +406,13 @@ class NativeLearner:
         self.device_shuffle = (env == "1") if env in ("0", "1") else (
             cfg.num_epochs * self.perm_n >= self.PERM_DEVICE_MIN)
         # look-ahead drafts in flight (FIFO), each chained on its predecessor's final RNG state;
-        # DPPO_PERM_DEPTH (default 3) of them, in the handle's 4 pinned slots beside the one the
-        # current learn uploads from -- a slow draw (host jitter) is absorbed instead of stalling
-        # the next learn.  (Two deep through round 5: a draft could only start once the slot
-        # whose upload was three learns back had landed, so on a loaded host -- draws 2-2.7 ms
-        # against a 3.6 ms device learn -- the draft thread idled between drafts and the C3
-        # learn went host-bound at ~230 M env-steps/s.)
+        # DPPO_PERM_DEPTH (default 2) of them, in the handle's 3 pinned slots beside the one the
+        # current learn uploads from -- two deep, a slow draw (host jitter) is absorbed instead
+        # of stalling the next learn.  (Round 6 measured 3 deep in 4 slots: 286.4 against 287.7 M
+        # env-steps/s at C3, 3 A/B pairs -- not kept.)
         self._drafts = collections.deque()
         self.draft_depth = max(1, min(N.PERM_SLOTS - 1,
-                                      int(os.environ.get("DPPO_PERM_DEPTH", "3"))))
+                                      int(os.environ.get("DPPO_PERM_DEPTH", "2"))))
         self._slot = 0
         self._worker = None
         self._closed = False

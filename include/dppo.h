@@ -232,14 +232,13 @@ int dppo_clip_adam_f32(float* params, float* grad, float* adam_m, float* adam_v,
                        float max_norm, double lr, float beta1, float beta2, float eps, int64_t step,
                        float* out_norm, void* stream);
 
-/* One of the handle's DPPO_PERM_SLOTS (4) pinned host staging buffers (slot 0..3) for the
+/* One of the handle's DPPO_PERM_SLOTS (3) pinned host staging buffers (slot 0..2) for the
  * [E][T*N] permutations or swap targets; waits for the previous learn's upload from that slot to
  * finish.  Generating straight into a slot (dppo_perm_numpy / dppo_perm_targets_numpy) and
  * passing it to dppo_learn_f32 / dppo_learn_targets_f32 makes the upload a pure asynchronous DMA;
- * four slots let the draws of the next three learns run on the host while the current learn's
- * upload is in flight (three until round 6: on a loaded host the draft thread then idled between
- * drafts, gated by the slot waits, and the learn went host-bound). */
-#define DPPO_PERM_SLOTS 4
+ * three slots let the draws of the next two learns run on the host while the current learn's
+ * upload is in flight. */
+#define DPPO_PERM_SLOTS 3
 int dppo_perm_buffer(dppo_handle* h, int32_t slot, int32_t** out);
 
 /* External staging slots (round 5): caller-owned host memory of `bytes` (e.g. a slot of a
