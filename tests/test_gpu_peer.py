@@ -80,6 +80,7 @@ def test_dead_peer_fails_loudly_within_the_timeout(tmp_path):
     r0, _ = _spawn("dead", tmp_path, env={"DPPO_PEER_TIMEOUT_S": "3"})
     err, again = str(r0["err"]), str(r0["again"])
     assert "peer exchange timed out" in err, err
+    assert "rank 1's word" in err, err   # the error word names the rank whose word never came
     assert "peer exchange timed out" in again, again
     assert float(r0["elapsed"]) < float(r0["timeout"]) + 10.0, float(r0["elapsed"])
 

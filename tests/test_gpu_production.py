@@ -261,7 +261,12 @@ def test_grid_fanin_reports_non_resident_grid():
     N.check(lib.dppo_fanin_selftest(h.h, cus + 8, 96 * 1024, 20_000, stream()))
     torch.cuda.synchronize()
     assert lib.dppo_status(h.h) == N.DPPO_EHIP
-    assert b"fan-in timed out" in lib.dppo_last_error()
+    msg = lib.dppo_last_error().decode()
+    assert "fan-in timed out" in msg
+    # the error word names the first wait that gave up: code 1, the workgroup that raised it
+    import re
+    hit = re.search(r"code 1, block (\d+)", msg)
+    assert hit and int(hit.group(1)) < cus + 8, msg
     rc = lib.dppo_learn_f32(h.h, ctypes.byref(st), pd.data_ptr(), m.data_ptr(), v.data_ptr(),
                             ctypes.byref(hp), perms.ctypes.data, None, stream())
     assert rc == N.DPPO_EHIP
