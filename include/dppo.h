@@ -361,7 +361,13 @@ int dppo_comm_init(dppo_handle* h, int32_t nranks, int32_t rank, const char* id1
  * it (run dppo_peer_selftest on every rank, agree on the results, dppo_peer_close on failure).
  * Waits are bounded by DPPO_PEER_TIMEOUT_S (default 60 s); a timeout makes dppo_status return
  * DPPO_ECOMM.  No reference counterpart (the reference is single-process); replaces the
- * torch.distributed all-reduce a data-parallel wrapper of ppo.py:276-285 would issue. */
+ * torch.distributed all-reduce a data-parallel wrapper of ppo.py:276-285 would issue.
+ * Exchange buffers (2 MiB each) are pooled for the life of the process: dppo_destroy returns the
+ * handle's buffer to the pool and the next dppo_peer_export of the same size, memory type and
+ * device takes it, zeroed (round 6: a buffer allocated where freed uncached ones had been lost a
+ * store).  A process uses ONE memory type (DPPO_PEER_MEM: uncached (default), fine or coarse); a
+ * second type fails with DPPO_EUNSUPPORTED.  Destroy every rank's handle of an exchange group
+ * before any rank exports again (a pooled buffer must not still be mapped by an old peer). */
 int dppo_peer_export(dppo_handle* h, unsigned char* out64);
 #define DPPO_PEER_SHARED_DEVICE 1 /* flags: some ranks share a GPU (keeps the exchange a kernel of
                                     its own instead of fusing it into the optimizer step, whose
