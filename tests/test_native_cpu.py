@@ -199,6 +199,30 @@ def test_parallel_draw_is_the_serial_draw(n, count, chunks, w):
             assert st["path"] == 1 and st["fail"] == 0, st  # the parallel draw itself ran
 
 
+@pytest.mark.parametrize("w", [0, 40])
+def test_two_drafts_as_one_parallel_draw_equal_the_chained_drafts(w):
+    """Cross-draft speculation in its simplest form (round 6, verdict r5 item 4): the MT19937 word
+    stream runs on from one learn's E permutations to the next, so ONE parallel draw of 2E epochs
+    -- chunk scans spanning the draft boundary, corrected by the same stitch -- gives exactly the
+    two chained E-epoch draws: targets, key and pos; with a forced narrow band (w = 40) the
+    stitch falls back to the serial draw and the result is still the same."""
+    n, E = (1 << 17) + 3, 4
+    rs = np.random.RandomState(31)
+    rs.random_sample(101)
+    key, pos, _ = N.mt_state(rs)
+    a = np.empty(n * E, np.int32)
+    b = np.empty(n * E, np.int32)
+    k1 = key.copy()
+    p1, _ = N.perm_targets_numpy_par(k1, pos, n, E, a, 1)
+    p1, _ = N.perm_targets_numpy_par(k1, p1, n, E, b, 1)
+    both = np.full(2 * n * E, -1, np.int32)
+    k2 = key.copy()
+    p2, st = N.perm_targets_numpy_par(k2, pos, n, 2 * E, both, 4, chunks=9, w=w)
+    assert np.array_equal(both[:n * E], a) and np.array_equal(both[n * E:], b), st
+    assert p2 == p1 and np.array_equal(k2, k1), st
+    assert st["path"] == (2 if w else 1), st
+
+
 def test_large_draws_take_the_parallel_path():
     """dppo_perm_targets_numpy at >= 2^22 targets runs the parallel draw by default; targets equal
     the serial draw's and the RNG ends where numpy's own permutations leave it."""
