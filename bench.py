@@ -507,6 +507,14 @@ def multi_gpu_report(world, rank, dist, device, steps, warmup):
         row["perm_device_ms_per_step"] = round(perm["ms_total"] / steps, 4) if perm else 0.0
         if not gmb:
             rep["exchange"] = exchange_report(agent, dist, device)
+        else:
+            # the node-shared draw (drawshare.py): per rank {shared, own, mismatch, timeout} --
+            # followers that took every draft from the leader drew nothing themselves
+            sh = agent._learner.share
+            mine = dict(sh.stats, leader=bool(sh.leader)) if sh is not None else None
+            allst = [None] * world
+            dist.all_gather_object(allst, mine)
+            row["perm_share"] = allst
         rep["c5_strong_" + ("global" if gmb else "local")] = row
         del agent
         torch.cuda.empty_cache()
